@@ -1,0 +1,222 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes binding of the CPU oracle (panda_oracle.c).
+
+The oracle is the fp64 CPU restatement the HIP path is checked against.  Only
+``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg
+import this module; the product package never does.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libpanda_oracle.so")
+
+TASKS = {"reach": 0, "push": 1, "pick_and_place": 2}
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("task", C.c_int32), ("control", C.c_int32), ("reward", C.c_int32), ("block_gripper", C.c_int32),
+        ("has_table", C.c_int32), ("has_plane", C.c_int32), ("has_cube", C.c_int32), ("has_robot", C.c_int32),
+        ("base", C.c_double * 3), ("cube_half", C.c_double), ("cube_mass", C.c_double),
+    ]
+
+
+class Env(C.Structure):
+    _fields_ = [
+        ("q", C.c_double * 9), ("qd", C.c_double * 9),
+        ("m_target", C.c_double * 9), ("m_kp", C.c_double * 9), ("m_kd", C.c_double * 9),
+        ("m_vel", C.c_double * 9), ("m_maximp", C.c_double * 9),
+        ("cpos", C.c_double * 3), ("cquat", C.c_double * 4), ("cvel", C.c_double * 3), ("comg", C.c_double * 3),
+        ("goal", C.c_double * 3), ("elapsed", C.c_int64), ("rng", C.c_uint64 * 4),
+    ]
+
+
+class Stats(C.Structure):
+    _fields_ = [("substeps", C.c_int64), ("pgs_iterations", C.c_int64), ("rows", C.c_int64), ("contacts", C.c_int64)]
+
+
+def build() -> str:
+    """Compile the oracle with its Makefile (gcc only)."""
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        P, D, I = C.POINTER, C.c_double, C.c_int
+        L.po_default_config.argtypes = [P(Config), I, I, I]
+        L.po_init_env.argtypes = [P(Config), P(Env)]
+        L.po_link_state.argtypes = [P(Config), P(Env), I, P(D), P(D), P(D), P(D)]
+        L.po_inverse_kinematics.argtypes = [P(Config), P(D), I, P(D), P(D), P(D)]
+        L.po_control_joints.argtypes = [P(Env), I, P(C.c_int32), P(D), P(D)]
+        L.po_substep.argtypes = [P(Config), P(Env), P(Stats)]
+        L.po_sim_step.argtypes = [P(Config), P(Env), P(Stats)]
+        L.po_euler_from_quaternion.argtypes = [P(D), P(D)]
+        L.po_obs_dim.argtypes = [P(Config)]
+        L.po_action_dim.argtypes = [P(Config)]
+        F, U8 = P(C.c_float), P(C.c_uint8)
+        L.po_reset.argtypes = [P(Config), P(Env), I, C.c_uint64, F, F, F]
+        L.po_get_obs.argtypes = [P(Config), P(Env), F, F, F]
+        L.po_step.argtypes = [P(Config), P(Env), F, F, F, F, F, U8, U8, I, F, F, P(Stats)]
+        L.po_step_batch.argtypes = [P(Config), P(Env), I, F, F, F, F, F, U8, U8, I, P(Stats)]
+        L.po_compute_reward.argtypes = [I, F, P(D)]
+        L.po_compute_reward.restype = C.c_float
+        L.po_is_success.argtypes = [F, P(D)]
+        L.po_is_success.restype = C.c_uint8
+        L.po_pcg64_seed.argtypes = [C.c_uint64, P(C.c_uint64)]
+        L.po_pcg64_next.argtypes = [P(C.c_uint64)]
+        L.po_pcg64_next.restype = C.c_uint64
+        L.po_pcg64_double.argtypes = [P(C.c_uint64)]
+        L.po_pcg64_double.restype = C.c_double
+        L.po_mass_matrix.argtypes = [P(Config), P(D), P(D)]
+        L.po_bias_forces.argtypes = [P(Config), P(D), P(D), P(D)]
+        L.po_link_inertia.argtypes = [I, P(D)]
+        L.po_set_link_aabb.argtypes = [I, D, D, D]
+        _lib = L
+    return _lib
+
+
+def _dp(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _fp(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def config(task="reach", control="ee", reward="sparse", **overrides) -> Config:
+    cfg = Config()
+    lib().po_default_config(C.byref(cfg), TASKS[task], 0 if control == "ee" else 1, 0 if reward == "sparse" else 1)
+    for k, v in overrides.items():
+        if k == "base":
+            for i in range(3):
+                cfg.base[i] = v[i]
+        else:
+            setattr(cfg, k, v)
+    return cfg
+
+
+def new_env(cfg: Config) -> Env:
+    env = Env()
+    lib().po_init_env(C.byref(cfg), C.byref(env))
+    return env
+
+
+def env_to_dict(env: Env) -> dict:
+    return {name: np.array(getattr(env, name)) if not isinstance(getattr(env, name), int) else getattr(env, name)
+            for name, _ in Env._fields_}
+
+
+def link_state(cfg, env, link):
+    pos, quat, v, w = np.zeros(3), np.zeros(4), np.zeros(3), np.zeros(3)
+    lib().po_link_state(C.byref(cfg), C.byref(env), link, _dp(pos), _dp(quat), _dp(v), _dp(w))
+    return pos, quat, v, w
+
+
+def inverse_kinematics(cfg, q_start, link, pos, orn):
+    q0 = np.ascontiguousarray(q_start, dtype=np.float64)
+    p = np.ascontiguousarray(pos, dtype=np.float64)
+    o = np.ascontiguousarray(orn, dtype=np.float64)
+    out = np.zeros(9)
+    lib().po_inverse_kinematics(C.byref(cfg), _dp(q0), link, _dp(p), _dp(o), _dp(out))
+    return out
+
+
+def control_joints(env, joints, targets, forces):
+    j = np.ascontiguousarray(joints, dtype=np.int32)
+    t = np.ascontiguousarray(targets, dtype=np.float64)
+    f = np.ascontiguousarray(forces, dtype=np.float64)
+    lib().po_control_joints(C.byref(env), len(j), j.ctypes.data_as(C.POINTER(C.c_int32)), _dp(t), _dp(f))
+
+
+def sim_step(cfg, env, stats: Stats | None = None):
+    lib().po_sim_step(C.byref(cfg), C.byref(env), C.byref(stats) if stats is not None else None)
+
+
+def obs_dim(cfg) -> int:
+    return lib().po_obs_dim(C.byref(cfg))
+
+
+def action_dim(cfg) -> int:
+    return lib().po_action_dim(C.byref(cfg))
+
+
+def reset(cfg, env, seed=None):
+    od = obs_dim(cfg)
+    obs, ag, dg = np.zeros(od, np.float32), np.zeros(3, np.float32), np.zeros(3, np.float32)
+    lib().po_reset(C.byref(cfg), C.byref(env), 0 if seed is None else 1, 0 if seed is None else int(seed),
+                   _fp(obs), _fp(ag), _fp(dg))
+    return obs, ag, dg
+
+
+def get_obs(cfg, env):
+    od = obs_dim(cfg)
+    obs, ag, dg = np.zeros(od, np.float32), np.zeros(3, np.float32), np.zeros(3, np.float32)
+    lib().po_get_obs(C.byref(cfg), C.byref(env), _fp(obs), _fp(ag), _fp(dg))
+    return obs, ag, dg
+
+
+def step(cfg, env, action, autoreset=False, stats: Stats | None = None):
+    od = obs_dim(cfg)
+    a = np.ascontiguousarray(action, dtype=np.float32)
+    obs, ag, dg = np.zeros(od, np.float32), np.zeros(3, np.float32), np.zeros(3, np.float32)
+    fo, fa = np.zeros(od, np.float32), np.zeros(3, np.float32)
+    r = np.zeros(1, np.float32)
+    te, tr = np.zeros(1, np.uint8), np.zeros(1, np.uint8)
+    lib().po_step(C.byref(cfg), C.byref(env), _fp(a), _fp(obs), _fp(ag), _fp(dg), _fp(r),
+                  te.ctypes.data_as(C.POINTER(C.c_uint8)), tr.ctypes.data_as(C.POINTER(C.c_uint8)),
+                  int(autoreset), _fp(fo), _fp(fa), C.byref(stats) if stats is not None else None)
+    return obs, ag, dg, float(r[0]), bool(te[0]), bool(tr[0])
+
+
+def compute_reward(reward_type: str, ag, dg):
+    a = np.ascontiguousarray(ag, dtype=np.float32)
+    d = np.ascontiguousarray(dg, dtype=np.float64)
+    return lib().po_compute_reward(0 if reward_type == "sparse" else 1, _fp(a), _dp(d))
+
+
+def is_success(ag, dg) -> bool:
+    a = np.ascontiguousarray(ag, dtype=np.float32)
+    d = np.ascontiguousarray(dg, dtype=np.float64)
+    return bool(lib().po_is_success(_fp(a), _dp(d)))
+
+
+def pcg64_seed(seed: int) -> np.ndarray:
+    st = np.zeros(4, np.uint64)
+    lib().po_pcg64_seed(C.c_uint64(seed), st.ctypes.data_as(C.POINTER(C.c_uint64)))
+    return st
+
+
+def pcg64_next(st: np.ndarray) -> int:
+    return int(lib().po_pcg64_next(st.ctypes.data_as(C.POINTER(C.c_uint64))))
+
+
+def mass_matrix(cfg, q):
+    qq = np.ascontiguousarray(q, dtype=np.float64)
+    M = np.zeros(81)
+    lib().po_mass_matrix(C.byref(cfg), _dp(qq), _dp(M))
+    return M.reshape(9, 9)
+
+
+def bias_forces(cfg, q, qd):
+    qq = np.ascontiguousarray(q, dtype=np.float64)
+    vv = np.ascontiguousarray(qd, dtype=np.float64)
+    h = np.zeros(9)
+    lib().po_bias_forces(C.byref(cfg), _dp(qq), _dp(vv), _dp(h))
+    return h
+
+
+def set_link_aabb(link, lx, ly, lz):
+    lib().po_set_link_aabb(link, lx, ly, lz)

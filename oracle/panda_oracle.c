@@ -1,0 +1,1171 @@
+/*
+ * panda_oracle.c — TEST INFRASTRUCTURE ONLY (see panda_oracle.h).
+ *
+ * Plain fp64 C, written for readability, not speed: dense 9x9 matrices,
+ * Jacobian-sum mass matrix, world-frame recursive Newton-Euler bias forces and
+ * a generic 15-DoF row solver.  The HIP product path re-derives the same
+ * algorithm independently in fp32 (panda-lang-manip_amd/csrc).
+ *
+ * Each function cites the reference call site (file:line under /root/reference)
+ * or the PyBullet 3.2.5 routine whose published behaviour it restates.
+ */
+#include "panda_oracle.h"
+
+#include <math.h>
+#include <string.h>
+
+#include "../include/panda_model.h"
+
+/* ------------------------------------------------------------------ model */
+typedef struct {
+    int parent, type, dof;
+    double origin[3], rpy[3], axis[3], Ro[9];
+    double mass, com[3], aabb[3], inertia[3];
+} olink;
+
+static olink L[PM_NUM_LINKS];
+static int dof_link[PM_NUM_DOFS];
+static double qlo[PM_NUM_DOFS], qhi[PM_NUM_DOFS];
+static unsigned anc[PM_NUM_LINKS];
+static int inited = 0;
+
+typedef struct {
+    int link;
+    double c[3], r, mu;
+} osphere;
+static osphere SPH[PM_NUM_SPHERES];
+
+static void rpy_to_mat(const double rpy[3], double R[9]) {
+    /* URDF: R = Rz(yaw) Ry(pitch) Rx(roll) */
+    double cr = cos(rpy[0]), sr = sin(rpy[0]), cp = cos(rpy[1]), sp = sin(rpy[1]), cy = cos(rpy[2]),
+           sy = sin(rpy[2]);
+    R[0] = cy * cp; R[1] = cy * sp * sr - sy * cr; R[2] = cy * sp * cr + sy * sr;
+    R[3] = sy * cp; R[4] = sy * sp * sr + cy * cr; R[5] = sy * sp * cr - cy * sr;
+    R[6] = -sp;     R[7] = cp * sr;                R[8] = cp * cr;
+}
+
+static void compute_inertia(olink *l) {
+    /* btCompoundShape::calculateLocalInertia: box of the AABB extents */
+    double lx = l->aabb[0], ly = l->aabb[1], lz = l->aabb[2];
+    l->inertia[0] = l->mass / 12.0 * (ly * ly + lz * lz);
+    l->inertia[1] = l->mass / 12.0 * (lx * lx + lz * lz);
+    l->inertia[2] = l->mass / 12.0 * (lx * lx + ly * ly);
+}
+
+static void model_init(void) {
+    if (inited) return;
+#define OL_LINK(idx, par, typ, ox, oy, oz, rr, pp, yy, ax, ay, az, dof_, m, cx, cy, cz, bx, by, bz) \
+    {                                                                                            \
+        olink *l = &L[idx];                                                                      \
+        l->parent = par; l->type = typ; l->dof = dof_;                                           \
+        l->origin[0] = ox; l->origin[1] = oy; l->origin[2] = oz;                                 \
+        l->rpy[0] = rr; l->rpy[1] = pp; l->rpy[2] = yy;                                          \
+        l->axis[0] = ax; l->axis[1] = ay; l->axis[2] = az;                                       \
+        l->mass = m; l->com[0] = cx; l->com[1] = cy; l->com[2] = cz;                             \
+        l->aabb[0] = bx; l->aabb[1] = by; l->aabb[2] = bz;                                       \
+    }
+    PM_LINK_TABLE(OL_LINK)
+#undef OL_LINK
+#define OL_DOF(d, link, lo, hi) \
+    dof_link[d] = link;         \
+    qlo[d] = lo;                \
+    qhi[d] = hi;
+    PM_DOF_TABLE(OL_DOF)
+#undef OL_DOF
+    {
+        int s = 0;
+#define OL_SPH(link_, x, y, z, rad, mu_) \
+    SPH[s].link = link_;                \
+    SPH[s].c[0] = x;                    \
+    SPH[s].c[1] = y;                    \
+    SPH[s].c[2] = z;                    \
+    SPH[s].r = rad;                     \
+    SPH[s].mu = mu_;                    \
+    s++;
+        PM_SPHERE_TABLE(OL_SPH)
+#undef OL_SPH
+    }
+    for (int i = 0; i < PM_NUM_LINKS; i++) {
+        rpy_to_mat(L[i].rpy, L[i].Ro);
+        compute_inertia(&L[i]);
+        anc[i] = 1u << i;
+        if (L[i].parent >= 0) anc[i] |= anc[L[i].parent];
+    }
+    inited = 1;
+}
+
+void po_link_inertia(int link, double inertia[3]) {
+    model_init();
+    memcpy(inertia, L[link].inertia, sizeof(double) * 3);
+}
+
+void po_set_link_aabb(int link, double lx, double ly, double lz) {
+    model_init();
+    L[link].aabb[0] = lx; L[link].aabb[1] = ly; L[link].aabb[2] = lz;
+    compute_inertia(&L[link]);
+}
+
+/* --------------------------------------------------------------- algebra */
+static void v3_cross(const double a[3], const double b[3], double o[3]) {
+    double x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
+    o[0] = x; o[1] = y; o[2] = z;
+}
+static double v3_dot(const double a[3], const double b[3]) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+static double v3_norm(const double a[3]) { return sqrt(v3_dot(a, a)); }
+static void m3_mul(const double A[9], const double B[9], double C[9]) {
+    double T[9];
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++) T[r * 3 + c] = A[r * 3] * B[c] + A[r * 3 + 1] * B[3 + c] + A[r * 3 + 2] * B[6 + c];
+    memcpy(C, T, sizeof T);
+}
+static void m3_vec(const double A[9], const double v[3], double o[3]) {
+    double x = A[0] * v[0] + A[1] * v[1] + A[2] * v[2];
+    double y = A[3] * v[0] + A[4] * v[1] + A[5] * v[2];
+    double z = A[6] * v[0] + A[7] * v[1] + A[8] * v[2];
+    o[0] = x; o[1] = y; o[2] = z;
+}
+static void m3_tvec(const double A[9], const double v[3], double o[3]) {
+    double x = A[0] * v[0] + A[3] * v[1] + A[6] * v[2];
+    double y = A[1] * v[0] + A[4] * v[1] + A[7] * v[2];
+    double z = A[2] * v[0] + A[5] * v[1] + A[8] * v[2];
+    o[0] = x; o[1] = y; o[2] = z;
+}
+/* Iw = R diag(I) R^T */
+static void inertia_world(const double R[9], const double I[3], double Iw[9]) {
+    for (int r = 0; r < 3; r++)
+        for (int c = 0; c < 3; c++)
+            Iw[r * 3 + c] = R[r * 3] * I[0] * R[c * 3] + R[r * 3 + 1] * I[1] * R[c * 3 + 1] +
+                            R[r * 3 + 2] * I[2] * R[c * 3 + 2];
+}
+
+/* btMatrix3x3::getRotation (Shepperd), quaternion (x,y,z,w) */
+static void mat_to_quat(const double m[9], double q[4]) {
+    double trace = m[0] + m[4] + m[8];
+    if (trace > 0.0) {
+        double s = sqrt(trace + 1.0);
+        q[3] = s * 0.5;
+        s = 0.5 / s;
+        q[0] = (m[7] - m[5]) * s;
+        q[1] = (m[2] - m[6]) * s;
+        q[2] = (m[3] - m[1]) * s;
+    } else {
+        int i = m[0] < m[4] ? (m[4] < m[8] ? 2 : 1) : (m[0] < m[8] ? 2 : 0);
+        int j = (i + 1) % 3, k = (i + 2) % 3;
+        double s = sqrt(m[i * 4] - m[j * 4] - m[k * 4] + 1.0);
+        q[i] = s * 0.5;
+        s = 0.5 / s;
+        q[3] = (m[k * 3 + j] - m[j * 3 + k]) * s;
+        q[j] = (m[j * 3 + i] + m[i * 3 + j]) * s;
+        q[k] = (m[k * 3 + i] + m[i * 3 + k]) * s;
+    }
+}
+
+static void quat_to_mat(const double q[4], double m[9]) {
+    double x = q[0], y = q[1], z = q[2], w = q[3];
+    double d = x * x + y * y + z * z + w * w, s = 2.0 / d;
+    double xs = x * s, ys = y * s, zs = z * s;
+    double wx = w * xs, wy = w * ys, wz = w * zs, xx = x * xs, xy = x * ys, xz = x * zs, yy = y * ys, yz = y * zs,
+           zz = z * zs;
+    m[0] = 1.0 - (yy + zz); m[1] = xy - wz;         m[2] = xz + wy;
+    m[3] = xy + wz;         m[4] = 1.0 - (xx + zz); m[5] = yz - wx;
+    m[6] = xz - wy;         m[7] = yz + wx;         m[8] = 1.0 - (xx + yy);
+}
+
+static void quat_mul(const double a[4], const double b[4], double o[4]) {
+    double x = a[3] * b[0] + a[0] * b[3] + a[1] * b[2] - a[2] * b[1];
+    double y = a[3] * b[1] + a[1] * b[3] + a[2] * b[0] - a[0] * b[2];
+    double z = a[3] * b[2] + a[2] * b[3] + a[0] * b[1] - a[1] * b[0];
+    double w = a[3] * b[3] - a[0] * b[0] - a[1] * b[1] - a[2] * b[2];
+    o[0] = x; o[1] = y; o[2] = z; o[3] = w;
+}
+
+/* ---------------------------------------------------------- kinematics */
+typedef struct {
+    double R[PM_NUM_LINKS][9], o[PM_NUM_LINKS][3], a[PM_NUM_LINKS][3], c[PM_NUM_LINKS][3];
+} okin;
+
+/* Link frames of the URDF tree; c[] = COM frame origin, which is what
+ * btMultiBody calls the link frame (getLinkState()[0], pybullet.py:361). */
+static void fk(const po_config *cfg, const double q[9], okin *k) {
+    static const double I3[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    for (int i = 0; i < PM_NUM_LINKS; i++) {
+        const olink *l = &L[i];
+        const double *Rp = l->parent < 0 ? I3 : k->R[l->parent];
+        const double *op = l->parent < 0 ? cfg->base : k->o[l->parent];
+        double Rj[9], oj[3];
+        m3_mul(Rp, l->Ro, Rj);
+        m3_vec(Rp, l->origin, oj);
+        oj[0] += op[0]; oj[1] += op[1]; oj[2] += op[2];
+        if (l->type == PM_JOINT_REVOLUTE) {
+            double th = q[l->dof], c = cos(th), s = sin(th);
+            double Rz[9] = {c, -s, 0, s, c, 0, 0, 0, 1};
+            m3_mul(Rj, Rz, k->R[i]);
+            memcpy(k->o[i], oj, sizeof oj);
+            m3_vec(Rj, l->axis, k->a[i]);
+        } else if (l->type == PM_JOINT_PRISMATIC) {
+            memcpy(k->R[i], Rj, sizeof Rj);
+            m3_vec(Rj, l->axis, k->a[i]);
+            for (int d = 0; d < 3; d++) k->o[i][d] = oj[d] + k->a[i][d] * q[l->dof];
+        } else {
+            memcpy(k->R[i], Rj, sizeof Rj);
+            memcpy(k->o[i], oj, sizeof oj);
+            k->a[i][0] = k->a[i][1] = k->a[i][2] = 0.0;
+        }
+        double cw[3];
+        m3_vec(k->R[i], l->com, cw);
+        for (int d = 0; d < 3; d++) k->c[i][d] = k->o[i][d] + cw[d];
+    }
+}
+
+/* Geometric Jacobian (world) of point p rigidly attached to `link`. */
+static void point_jac(const okin *k, int link, const double p[3], double Jv[3][9], double Jw[3][9]) {
+    for (int d = 0; d < PM_NUM_DOFS; d++) {
+        int j = dof_link[d];
+        double lin[3] = {0, 0, 0}, ang[3] = {0, 0, 0};
+        if (anc[link] & (1u << j)) {
+            if (L[j].type == PM_JOINT_REVOLUTE) {
+                double r[3] = {p[0] - k->o[j][0], p[1] - k->o[j][1], p[2] - k->o[j][2]};
+                v3_cross(k->a[j], r, lin);
+                memcpy(ang, k->a[j], sizeof ang);
+            } else {
+                memcpy(lin, k->a[j], sizeof lin);
+            }
+        }
+        for (int r = 0; r < 3; r++) {
+            Jv[r][d] = lin[r];
+            Jw[r][d] = ang[r];
+        }
+    }
+}
+
+void po_link_state(const po_config *cfg, const po_env *env, int link, double pos[3], double quat[4],
+                   double lin_vel[3], double ang_vel[3]) {
+    /* getLinkState(body, link, computeLinkVelocity=1): [0] COM position,
+     * [1] COM-frame orientation, [6] linear, [7] angular velocity
+     * (pybullet.py:351-400). */
+    model_init();
+    okin k;
+    fk(cfg, env->q, &k);
+    memcpy(pos, k.c[link], sizeof(double) * 3);
+    mat_to_quat(k.R[link], quat);
+    double Jv[3][9], Jw[3][9];
+    point_jac(&k, link, k.c[link], Jv, Jw);
+    for (int r = 0; r < 3; r++) {
+        lin_vel[r] = ang_vel[r] = 0.0;
+        for (int d = 0; d < 9; d++) {
+            lin_vel[r] += Jv[r][d] * env->qd[d];
+            ang_vel[r] += Jw[r][d] * env->qd[d];
+        }
+    }
+}
+
+/* ------------------------------------------------------------- dynamics */
+static void mass_matrix(const okin *k, double M[81]) {
+    memset(M, 0, sizeof(double) * 81);
+    for (int i = 0; i < PM_NUM_LINKS; i++) {
+        if (L[i].mass <= 0.0) continue;
+        double Jv[3][9], Jw[3][9], Iw[9];
+        point_jac(k, i, k->c[i], Jv, Jw);
+        inertia_world(k->R[i], L[i].inertia, Iw);
+        for (int a = 0; a < 9; a++)
+            for (int b = 0; b < 9; b++) {
+                double s = 0.0;
+                for (int r = 0; r < 3; r++) {
+                    s += L[i].mass * Jv[r][a] * Jv[r][b];
+                    for (int c = 0; c < 3; c++) s += Jw[r][a] * Iw[r * 3 + c] * Jw[c][b];
+                }
+                M[a * 9 + b] += s;
+            }
+    }
+}
+
+/* h(q,qd) = C qd + g + btMultiBody link damping, via world-frame RNEA with
+ * qdd = 0 (btMultiBody::computeAccelerationsArticulatedBodyAlgorithmMultiDof:
+ * gyroscopic term, gravity as link force, damping k1+k2|v| on every link). */
+static void bias_forces(const okin *k, const double qd[9], double h[9]) {
+    double w[PM_NUM_LINKS][3], dw[PM_NUM_LINKS][3], vo[PM_NUM_LINKS][3], ao[PM_NUM_LINKS][3];
+    double f[PM_NUM_LINKS][3], n[PM_NUM_LINKS][3];
+    const double zero[3] = {0, 0, 0}, agrav[3] = {0, 0, -PM_GRAVITY_Z};
+    for (int i = 0; i < PM_NUM_LINKS; i++) {
+        const olink *l = &L[i];
+        int p = l->parent;
+        const double *wp = p < 0 ? zero : w[p], *dwp = p < 0 ? zero : dw[p], *vp = p < 0 ? zero : vo[p],
+                     *ap = p < 0 ? agrav : ao[p];
+        const double *op = p < 0 ? k->o[i] : k->o[p]; /* base origin coincides with link-0 joint frame offset */
+        double r[3];
+        if (p < 0) {
+            r[0] = r[1] = r[2] = 0.0; /* fixed base: its velocity/acceleration fields are uniform */
+        } else {
+            r[0] = k->o[i][0] - op[0]; r[1] = k->o[i][1] - op[1]; r[2] = k->o[i][2] - op[2];
+        }
+        double t[3], t2[3];
+        double qdi = l->dof >= 0 ? qd[l->dof] : 0.0;
+        /* angular */
+        for (int d = 0; d < 3; d++) { w[i][d] = wp[d]; dw[i][d] = dwp[d]; }
+        if (l->type == PM_JOINT_REVOLUTE) {
+            v3_cross(wp, k->a[i], t);
+            for (int d = 0; d < 3; d++) { w[i][d] += k->a[i][d] * qdi; dw[i][d] += t[d] * qdi; }
+        }
+        /* linear at frame origin */
+        v3_cross(wp, r, t);
+        for (int d = 0; d < 3; d++) vo[i][d] = vp[d] + t[d];
+        v3_cross(dwp, r, t);
+        v3_cross(wp, r, t2);
+        double t3[3];
+        v3_cross(wp, t2, t3);
+        for (int d = 0; d < 3; d++) ao[i][d] = ap[d] + t[d] + t3[d];
+        if (l->type == PM_JOINT_PRISMATIC) {
+            v3_cross(wp, k->a[i], t);
+            for (int d = 0; d < 3; d++) { vo[i][d] += k->a[i][d] * qdi; ao[i][d] += 2.0 * t[d] * qdi; }
+        }
+        /* COM */
+        double rc[3] = {k->c[i][0] - k->o[i][0], k->c[i][1] - k->o[i][1], k->c[i][2] - k->o[i][2]};
+        double vc[3], ac[3];
+        v3_cross(w[i], rc, t);
+        for (int d = 0; d < 3; d++) vc[d] = vo[i][d] + t[d];
+        v3_cross(dw[i], rc, t);
+        v3_cross(w[i], rc, t2);
+        v3_cross(w[i], t2, t3);
+        for (int d = 0; d < 3; d++) ac[d] = ao[i][d] + t[d] + t3[d];
+        double Iw[9], Iww[3], Idw[3], gyro[3];
+        inertia_world(k->R[i], l->inertia, Iw);
+        m3_vec(Iw, w[i], Iww);
+        m3_vec(Iw, dw[i], Idw);
+        v3_cross(w[i], Iww, gyro);
+        double cl = PM_LINEAR_DAMPING + PM_LINEAR_DAMPING * v3_norm(vc);
+        double ca = PM_ANGULAR_DAMPING + PM_ANGULAR_DAMPING * v3_norm(w[i]);
+        double F[3], N[3];
+        for (int d = 0; d < 3; d++) {
+            F[d] = l->mass * ac[d] + l->mass * vc[d] * cl;
+            N[d] = Idw[d] + gyro[d] + Iww[d] * ca;
+        }
+        v3_cross(rc, F, t);
+        for (int d = 0; d < 3; d++) { f[i][d] = F[d]; n[i][d] = N[d] + t[d]; }
+    }
+    for (int i = PM_NUM_LINKS - 1; i >= 0; i--) {
+        const olink *l = &L[i];
+        if (l->type == PM_JOINT_REVOLUTE) h[l->dof] = v3_dot(k->a[i], n[i]);
+        else if (l->type == PM_JOINT_PRISMATIC) h[l->dof] = v3_dot(k->a[i], f[i]);
+        int p = l->parent;
+        if (p >= 0) {
+            double r[3] = {k->o[i][0] - k->o[p][0], k->o[i][1] - k->o[p][1], k->o[i][2] - k->o[p][2]}, t[3];
+            v3_cross(r, f[i], t);
+            for (int d = 0; d < 3; d++) { f[p][d] += f[i][d]; n[p][d] += n[i][d] + t[d]; }
+        }
+    }
+}
+
+void po_mass_matrix(const po_config *cfg, const double q[9], double M[81]) {
+    model_init();
+    okin k;
+    fk(cfg, q, &k);
+    mass_matrix(&k, M);
+}
+
+void po_bias_forces(const po_config *cfg, const double q[9], const double qd[9], double h[9]) {
+    model_init();
+    okin k;
+    fk(cfg, q, &k);
+    bias_forces(&k, qd, h);
+}
+
+/* SPD inverse by Cholesky (the oracle only needs a correct M^-1). */
+static void spd_inverse(const double A[81], double Ai[81]) {
+    double Lc[81];
+    memset(Lc, 0, sizeof Lc);
+    for (int i = 0; i < 9; i++)
+        for (int j = 0; j <= i; j++) {
+            double s = A[i * 9 + j];
+            for (int k = 0; k < j; k++) s -= Lc[i * 9 + k] * Lc[j * 9 + k];
+            if (i == j) Lc[i * 9 + i] = sqrt(s);
+            else Lc[i * 9 + j] = s / Lc[j * 9 + j];
+        }
+    for (int c = 0; c < 9; c++) {
+        double y[9], x[9];
+        for (int i = 0; i < 9; i++) {
+            double s = (i == c) ? 1.0 : 0.0;
+            for (int k = 0; k < i; k++) s -= Lc[i * 9 + k] * y[k];
+            y[i] = s / Lc[i * 9 + i];
+        }
+        for (int i = 8; i >= 0; i--) {
+            double s = y[i];
+            for (int k = i + 1; k < 9; k++) s -= Lc[k * 9 + i] * x[k];
+            x[i] = s / Lc[i * 9 + i];
+        }
+        for (int i = 0; i < 9; i++) Ai[i * 9 + c] = x[i];
+    }
+}
+
+/* Gaussian elimination with partial pivoting (MatrixRmn::Solve). */
+static void ge_solve(int n, double *A, double *b, double *x) {
+    for (int c = 0; c < n; c++) {
+        int piv = c;
+        for (int r = c + 1; r < n; r++)
+            if (fabs(A[r * n + c]) > fabs(A[piv * n + c])) piv = r;
+        if (piv != c) {
+            for (int k = 0; k < n; k++) { double t = A[c * n + k]; A[c * n + k] = A[piv * n + k]; A[piv * n + k] = t; }
+            double t = b[c]; b[c] = b[piv]; b[piv] = t;
+        }
+        for (int r = c + 1; r < n; r++) {
+            double f = A[r * n + c] / A[c * n + c];
+            for (int k = c; k < n; k++) A[r * n + k] -= f * A[c * n + k];
+            b[r] -= f * b[c];
+        }
+    }
+    for (int r = n - 1; r >= 0; r--) {
+        double s = b[r];
+        for (int k = r + 1; k < n; k++) s -= A[r * n + k] * x[k];
+        x[r] = s / A[r * n + r];
+    }
+}
+
+/* ------------------------------------------------------ inverse kinematics
+ * PyBullet calculateInverseKinematics (pybullet.py:479-497 -> PhysicsServer
+ * CommandProcessor IK loop + IKTrajectoryHelper::computeIK, IK2_VEL_DLS_WITH_
+ * ORIENTATION): up to 20 iterations while |p_ee - p*| > 1e-4, each one a damped
+ * least-squares step dq = (J^T J + diag(0.5))^-1 J^T [dp; dr] clamped to
+ * 45 deg max component, with the orientation error from
+ * deltaQ = q* x q_ee^-1 (angle kept in float as in computeIK). */
+void po_inverse_kinematics(const po_config *cfg, const double q_start[9], int link, const double pos[3],
+                           const double orn[4], double q_out[9]) {
+    model_init();
+    double q[9];
+    memcpy(q, q_start, sizeof q);
+    /* the target orientation goes through a btTransform (setRotation ->
+     * getRotation), which normalises it */
+    double on = sqrt(orn[0] * orn[0] + orn[1] * orn[1] + orn[2] * orn[2] + orn[3] * orn[3]);
+    double ot[4] = {orn[0] / on, orn[1] / on, orn[2] / on, orn[3] / on};
+    double diff = 1e30;
+    for (int it = 0; it < PM_IK_MAX_ITERS && diff > PM_IK_RESIDUAL; it++) {
+        okin k;
+        fk(cfg, q, &k);
+        /* btMultiBodyTreeCreator places each body frame at the joint pivot
+         * (URDF link frame), so IK drives the link-frame origin. */
+        const double *p = k.o[link];
+        double Jv[3][9], Jw[3][9];
+        point_jac(&k, link, p, Jv, Jw);
+        double dS[3] = {pos[0] - p[0], pos[1] - p[1], pos[2] - p[2]};
+        diff = v3_norm(dS);
+        double qe[4];
+        mat_to_quat(k.R[link], qe);
+        double n2 = qe[0] * qe[0] + qe[1] * qe[1] + qe[2] * qe[2] + qe[3] * qe[3];
+        double qinv[4] = {-qe[0] / n2, -qe[1] / n2, -qe[2] / n2, qe[3] / n2};
+        double dq[4];
+        quat_mul(ot, qinv, dq);
+        double wc = dq[3] < -1.0 ? -1.0 : (dq[3] > 1.0 ? 1.0 : dq[3]);
+        float angle = (float)(2.0 * acos(wc));
+        double s2 = 1.0 - dq[3] * dq[3], ax[3];
+        if (s2 < 10.0 * 2.2204460492503131e-16) {
+            ax[0] = 1.0; ax[1] = 0.0; ax[2] = 0.0;
+        } else {
+            double s = 1.0 / sqrt(s2);
+            ax[0] = dq[0] * s; ax[1] = dq[1] * s; ax[2] = dq[2] * s;
+        }
+        if (angle > 3.14159265358979323846) angle -= (float)(2.0 * 3.14159265358979323846);
+        else if (angle < -3.14159265358979323846) angle += (float)(2.0 * 3.14159265358979323846);
+        double an = v3_norm(ax);
+        double dR[3] = {angle * ax[0] / an, angle * ax[1] / an, angle * ax[2] / an};
+        double dC[6] = {dS[0], dS[1], dS[2], dR[0], dR[1], dR[2]};
+        double J[6][9];
+        for (int r = 0; r < 3; r++)
+            for (int d = 0; d < 9; d++) { J[r][d] = Jv[r][d]; J[r + 3][d] = Jw[r][d]; }
+        double U[81], rhs[9], dth[9];
+        for (int a = 0; a < 9; a++) {
+            rhs[a] = 0.0;
+            for (int r = 0; r < 6; r++) rhs[a] += J[r][a] * dC[r];
+            for (int b = 0; b < 9; b++) {
+                double s = 0.0;
+                for (int r = 0; r < 6; r++) s += J[r][a] * J[r][b];
+                U[a * 9 + b] = s + (a == b ? PM_IK_DAMPING : 0.0);
+            }
+        }
+        ge_solve(9, U, rhs, dth);
+        double mx = 0.0;
+        for (int d = 0; d < 9; d++) if (fabs(dth[d]) > mx) mx = fabs(dth[d]);
+        if (mx > PM_IK_MAX_ANGLE)
+            for (int d = 0; d < 9; d++) dth[d] *= PM_IK_MAX_ANGLE / mx;
+        for (int d = 0; d < 9; d++) q[d] += dth[d];
+    }
+    memcpy(q_out, q, sizeof q);
+}
+
+/* ---------------------------------------------------------- constraints */
+#define ND 15 /* robot 9 + cube [omega(3), v(3)], world frame */
+#define MAX_ROWS 128
+#define MAX_CONTACTS 32
+
+typedef struct {
+    double J[ND], MJ[ND];
+    double rhs, lo, hi, lam, dinv, mu;
+    int normal; /* for friction rows: index of the normal row */
+} orow;
+
+typedef struct {
+    int bodyA; /* robot link index, or -2 = cube */
+    int bodyB; /* -2 = cube, -1 = static */
+    double pA[3], pB[3], n[3], dist, mu;
+} ocontact;
+
+/* btPlaneSpace1 */
+static void plane_space(const double n[3], double p[3], double q[3]) {
+    if (fabs(n[2]) > 0.7071067811865475244) {
+        double a = n[1] * n[1] + n[2] * n[2], k = 1.0 / sqrt(a);
+        p[0] = 0; p[1] = -n[2] * k; p[2] = n[1] * k;
+        q[0] = a * k; q[1] = -n[0] * p[2]; q[2] = n[0] * p[1];
+    } else {
+        double a = n[0] * n[0] + n[1] * n[1], k = 1.0 / sqrt(a);
+        p[0] = -n[1] * k; p[1] = n[0] * k; p[2] = 0;
+        q[0] = -n[2] * p[1]; q[1] = n[2] * p[0]; q[2] = a * k;
+    }
+}
+
+static int ground_top(const po_config *cfg, double x, double y, double *top) {
+    if (cfg->has_table && fabs(x - PM_TABLE_CX) <= PM_TABLE_HX && fabs(y) <= PM_TABLE_HY) {
+        *top = PM_TABLE_TOP;
+        return 1;
+    }
+    if (cfg->has_plane) {
+        *top = PM_PLANE_TOP;
+        return 1;
+    }
+    return 0;
+}
+
+/* Contact generation (replaces Bullet's broadphase + box-box / convex
+ * narrowphase with the proxies of panda_model.h), fixed order:
+ *   1. gripper spheres vs cube (closest point on the cube)
+ *   2. cube vertices vs ground (table top or plane), first 4 in vertex order
+ *   3. gripper spheres vs ground */
+static int gen_contacts(const po_config *cfg, const po_env *env, const okin *k, ocontact *out) {
+    int nc = 0;
+    double Rc[9];
+    if (cfg->has_cube) quat_to_mat(env->cquat, Rc);
+    double sc[PM_NUM_SPHERES][3];
+    if (cfg->has_robot)
+        for (int s = 0; s < PM_NUM_SPHERES; s++) {
+            double t[3];
+            m3_vec(k->R[SPH[s].link], SPH[s].c, t);
+            for (int d = 0; d < 3; d++) sc[s][d] = k->o[SPH[s].link][d] + t[d];
+        }
+    if (cfg->has_cube && cfg->has_robot) {
+        double h = cfg->cube_half;
+        for (int s = 0; s < PM_NUM_SPHERES; s++) {
+            double rel[3] = {sc[s][0] - env->cpos[0], sc[s][1] - env->cpos[1], sc[s][2] - env->cpos[2]}, loc[3];
+            m3_tvec(Rc, rel, loc);
+            double cl[3], dif[3], nl[3], dist;
+            for (int d = 0; d < 3; d++) {
+                cl[d] = loc[d] < -h ? -h : (loc[d] > h ? h : loc[d]);
+                dif[d] = loc[d] - cl[d];
+            }
+            double dn = v3_norm(dif);
+            if (dn > 1e-9) {
+                for (int d = 0; d < 3; d++) nl[d] = dif[d] / dn;
+                dist = dn - SPH[s].r;
+            } else {
+                int ax = 0;
+                double best = h - fabs(loc[0]);
+                for (int d = 1; d < 3; d++)
+                    if (h - fabs(loc[d]) < best) { best = h - fabs(loc[d]); ax = d; }
+                nl[0] = nl[1] = nl[2] = 0.0;
+                nl[ax] = loc[ax] >= 0.0 ? 1.0 : -1.0;
+                cl[ax] = nl[ax] * h;
+                dist = -best - SPH[s].r;
+            }
+            if (dist < PM_CONTACT_MARGIN_SPHERE) {
+                ocontact *c = &out[nc++];
+                c->bodyA = SPH[s].link;
+                c->bodyB = -2;
+                m3_vec(Rc, nl, c->n);
+                double pw[3];
+                m3_vec(Rc, cl, pw);
+                for (int d = 0; d < 3; d++) {
+                    c->pB[d] = env->cpos[d] + pw[d];
+                    c->pA[d] = sc[s][d] - c->n[d] * SPH[s].r;
+                }
+                c->dist = dist;
+                c->mu = SPH[s].mu * PM_DEFAULT_FRICTION;
+            }
+        }
+    }
+    if (cfg->has_cube) {
+        double h = cfg->cube_half;
+        int ng = 0;
+        for (int v = 0; v < 8 && ng < 4; v++) {
+            double loc[3] = {(v & 1) ? h : -h, (v & 2) ? h : -h, (v & 4) ? h : -h}, pw[3];
+            m3_vec(Rc, loc, pw);
+            for (int d = 0; d < 3; d++) pw[d] += env->cpos[d];
+            double top;
+            if (!ground_top(cfg, pw[0], pw[1], &top)) continue;
+            double dist = pw[2] - top;
+            if (dist < PM_CONTACT_MARGIN_GROUND) {
+                ocontact *c = &out[nc++];
+                ng++;
+                c->bodyA = -2;
+                c->bodyB = -1;
+                c->n[0] = 0; c->n[1] = 0; c->n[2] = 1;
+                memcpy(c->pA, pw, sizeof pw);
+                c->pB[0] = pw[0]; c->pB[1] = pw[1]; c->pB[2] = top;
+                c->dist = dist;
+                c->mu = PM_DEFAULT_FRICTION * PM_DEFAULT_FRICTION;
+            }
+        }
+    }
+    if (cfg->has_robot) {
+        for (int s = 0; s < PM_NUM_SPHERES; s++) {
+            double top;
+            if (!ground_top(cfg, sc[s][0], sc[s][1], &top)) continue;
+            double dist = sc[s][2] - SPH[s].r - top;
+            if (dist < PM_CONTACT_MARGIN_SPHERE) {
+                ocontact *c = &out[nc++];
+                c->bodyA = SPH[s].link;
+                c->bodyB = -1;
+                c->n[0] = 0; c->n[1] = 0; c->n[2] = 1;
+                c->pA[0] = sc[s][0]; c->pA[1] = sc[s][1]; c->pA[2] = sc[s][2] - SPH[s].r;
+                c->pB[0] = sc[s][0]; c->pB[1] = sc[s][1]; c->pB[2] = top;
+                c->dist = dist;
+                c->mu = SPH[s].mu * PM_DEFAULT_FRICTION;
+            }
+        }
+    }
+    return nc;
+}
+
+/* Jacobian of one contact row along direction n (world): A gets +n, B gets -n. */
+static void contact_row_jac(const okin *k, const po_env *env, const ocontact *c, const double n[3], double J[ND]) {
+    memset(J, 0, sizeof(double) * ND);
+    for (int side = 0; side < 2; side++) {
+        int body = side ? c->bodyB : c->bodyA;
+        double sg = side ? -1.0 : 1.0;
+        const double *p = side ? c->pB : c->pA;
+        if (body >= 0) {
+            double Jv[3][9], Jw[3][9];
+            point_jac(k, body, p, Jv, Jw);
+            for (int d = 0; d < 9; d++) J[d] += sg * (n[0] * Jv[0][d] + n[1] * Jv[1][d] + n[2] * Jv[2][d]);
+        } else if (body == -2) {
+            double r[3] = {p[0] - env->cpos[0], p[1] - env->cpos[1], p[2] - env->cpos[2]}, rn[3];
+            v3_cross(r, n, rn);
+            for (int d = 0; d < 3; d++) {
+                J[9 + d] += sg * rn[d];
+                J[12 + d] += sg * n[d];
+            }
+        }
+    }
+}
+
+static double row_dot(const double *a, const double *b) {
+    double s = 0.0;
+    for (int d = 0; d < ND; d++) s += a[d] * b[d];
+    return s;
+}
+
+/* resolveSingleConstraintRowGeneric */
+static double solve_row(orow *r, double dv[ND]) {
+    if (r->dinv == 0.0) return 0.0;
+    double dl = r->rhs - r->dinv * row_dot(r->J, dv);
+    double sum = r->lam + dl;
+    if (sum < r->lo) { dl = r->lo - r->lam; r->lam = r->lo; }
+    else if (sum > r->hi) { dl = r->hi - r->lam; r->lam = r->hi; }
+    else r->lam = sum;
+    for (int d = 0; d < ND; d++) dv[d] += r->MJ[d] * dl;
+    return dl / r->dinv;
+}
+
+/* resolveConeFrictionConstraintRows: both directions from the same dv, then
+ * the pair is projected onto the disk |f| <= mu * lambda_n. */
+static double solve_cone(orow *a, orow *b, double lam_n, double dv[ND]) {
+    double dla = a->rhs - a->dinv * row_dot(a->J, dv);
+    double dlb = b->rhs - b->dinv * row_dot(b->J, dv);
+    double sa = a->lam + dla, sb = b->lam + dlb;
+    double lim = a->mu * (lam_n > 0.0 ? lam_n : 0.0);
+    double mag = sqrt(sa * sa + sb * sb);
+    if (mag > lim) {
+        double s = mag > 0.0 ? lim / mag : 0.0;
+        sa *= s;
+        sb *= s;
+    }
+    dla = sa - a->lam;
+    dlb = sb - b->lam;
+    a->lam = sa;
+    b->lam = sb;
+    for (int d = 0; d < ND; d++) dv[d] += a->MJ[d] * dla + b->MJ[d] * dlb;
+    double ra = a->dinv != 0.0 ? dla / a->dinv : 0.0, rb = b->dinv != 0.0 ? dlb / b->dinv : 0.0;
+    return fabs(ra) > fabs(rb) ? ra : rb;
+}
+
+static void finish_row(orow *r, const double Minv_r[81], double cube_inv_I, double cube_inv_m, const double v1[ND]) {
+    for (int a = 0; a < 9; a++) {
+        double s = 0.0;
+        for (int b = 0; b < 9; b++) s += Minv_r[a * 9 + b] * r->J[b];
+        r->MJ[a] = s;
+    }
+    for (int d = 0; d < 3; d++) {
+        r->MJ[9 + d] = r->J[9 + d] * cube_inv_I;
+        r->MJ[12 + d] = r->J[12 + d] * cube_inv_m;
+    }
+    double den = row_dot(r->J, r->MJ);
+    r->dinv = den > 2.2204460492503131e-16 ? 1.0 / den : 0.0;
+    r->lam = 0.0;
+    (void)v1;
+}
+
+/* One btMultiBodyDynamicsWorld::stepSimulation of 1/500 s
+ * (pybullet.py:52-55 calls it 20 times per env step):
+ *   1. forward dynamics velocity update qd1 = qd + h M^-1 (-bias)
+ *   2. constraint rows at the current positions: joint limits, joint motors,
+ *      contacts (normal + 2 friction directions)
+ *   3. projected Gauss-Seidel, 50 iterations or max residual^2 <= 1e-7,
+ *      non-contact rows in alternating order, then normals, then friction
+ *   4. semi-implicit integration of q and of the cube pose (exp map). */
+void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
+    model_init();
+    const double dt = PM_TIMESTEP;
+    okin k;
+    double Minv[81];
+    double v1[ND];
+    memset(v1, 0, sizeof v1);
+    memset(Minv, 0, sizeof Minv);
+    if (cfg->has_robot) {
+        fk(cfg, env->q, &k);
+        double M[81], hb[9];
+        mass_matrix(&k, M);
+        bias_forces(&k, env->qd, hb);
+        spd_inverse(M, Minv);
+        for (int a = 0; a < 9; a++) {
+            double s = 0.0;
+            for (int b = 0; b < 9; b++) s -= Minv[a * 9 + b] * hb[b];
+            v1[a] = env->qd[a] + dt * s;
+        }
+    }
+    double cube_I = 0.0, inv_I = 0.0, inv_m = 0.0;
+    if (cfg->has_cube) {
+        double l = 2.0 * cfg->cube_half;
+        cube_I = cfg->cube_mass / 12.0 * (l * l + l * l);
+        inv_I = 1.0 / cube_I;
+        inv_m = 1.0 / cfg->cube_mass;
+        double cl = PM_LINEAR_DAMPING + PM_LINEAR_DAMPING * v3_norm(env->cvel);
+        double ca = PM_ANGULAR_DAMPING + PM_ANGULAR_DAMPING * v3_norm(env->comg);
+        for (int d = 0; d < 3; d++) {
+            double g = d == 2 ? PM_GRAVITY_Z : 0.0;
+            v1[12 + d] = env->cvel[d] + dt * (g - cl * env->cvel[d]);
+            v1[9 + d] = env->comg[d] + dt * (-ca * env->comg[d]);
+        }
+    }
+
+    static orow rows[MAX_ROWS];
+    int nr = 0;
+    /* deep joint-limit violations are solved in split-impulse mode: the
+     * velocity row only stops further violation and the position error is
+     * removed by a position-only correction (PM_SPLIT_LIMIT_ERP per substep) */
+    double split_dq[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    int n_noncontact = 0;
+    if (cfg->has_robot) {
+        /* btMultiBodyJointLimitConstraint::createConstraintRows (lower row,
+         * upper row; only when the limit is touched or violated) */
+        for (int d = 0; d < 9; d++) {
+            for (int side = 0; side < 2; side++) {
+                double pen = side ? qhi[d] - env->q[d] : env->q[d] - qlo[d];
+                if (pen > 0.0) continue;
+                orow *r = &rows[nr++];
+                memset(r, 0, sizeof *r);
+                r->J[d] = side ? -1.0 : 1.0;
+                finish_row(r, Minv, inv_I, inv_m, v1);
+                double rel = row_dot(r->J, v1);
+                double velerr = -rel, poserr = 0.0;
+                int combined = pen > PM_SPLIT_PENETRATION_THRESHOLD;
+                poserr = -pen * PM_ERP / dt;
+                r->rhs = combined ? (poserr + velerr) * r->dinv : velerr * r->dinv;
+                if (!combined) split_dq[d] += r->J[d] * (-pen) * PM_SPLIT_LIMIT_ERP;
+                r->lo = 0.0;
+                r->hi = PM_LIMIT_MAX_IMPULSE;
+                r->normal = -1;
+            }
+        }
+        /* btMultiBodyJointMotor::createConstraintRows */
+        for (int d = 0; d < 9; d++) {
+            if (env->m_maximp[d] == 0.0) continue;
+            orow *r = &rows[nr++];
+            memset(r, 0, sizeof *r);
+            r->J[d] = 1.0;
+            finish_row(r, Minv, inv_I, inv_m, v1);
+            double cur = v1[d];
+            double target = env->m_kp[d] * (env->m_target[d] - env->q[d]) / dt + cur +
+                            env->m_kd[d] * (env->m_vel[d] - cur);
+            r->rhs = (target - cur) * r->dinv;
+            r->lo = -env->m_maximp[d];
+            r->hi = env->m_maximp[d];
+            r->normal = -1;
+        }
+    }
+    n_noncontact = nr;
+
+    ocontact cts[MAX_CONTACTS];
+    int nc = gen_contacts(cfg, env, &k, cts);
+    int normal_base = nr;
+    for (int c = 0; c < nc; c++) {
+        orow *r = &rows[nr++];
+        memset(r, 0, sizeof *r);
+        contact_row_jac(&k, env, &cts[c], cts[c].n, r->J);
+        finish_row(r, Minv, inv_I, inv_m, v1);
+        double rel = row_dot(r->J, v1);
+        double pen = cts[c].dist + PM_LINEAR_SLOP;
+        double velerr = -rel, poserr = 0.0;
+        if (pen > 0.0) velerr -= pen / dt;
+        else poserr = -pen * PM_ERP / dt;
+        int combined = pen > PM_SPLIT_PENETRATION_THRESHOLD;
+        r->rhs = combined ? (poserr + velerr) * r->dinv : velerr * r->dinv;
+        r->lo = 0.0;
+        r->hi = PM_CONTACT_UPPER;
+        r->normal = -1;
+    }
+    int fric_base = nr;
+    for (int c = 0; c < nc; c++) {
+        double t1[3], t2[3];
+        plane_space(cts[c].n, t1, t2);
+        for (int f = 0; f < 2; f++) {
+            orow *r = &rows[nr++];
+            memset(r, 0, sizeof *r);
+            contact_row_jac(&k, env, &cts[c], f ? t2 : t1, r->J);
+            finish_row(r, Minv, inv_I, inv_m, v1);
+            r->rhs = -row_dot(r->J, v1) * r->dinv;
+            r->mu = cts[c].mu;
+            r->normal = normal_base + c;
+        }
+    }
+
+    double dv[ND];
+    memset(dv, 0, sizeof dv);
+    int it;
+    for (it = 0; it < PM_SOLVER_ITERATIONS; it++) {
+        double res = 0.0, x;
+        for (int j = 0; j < n_noncontact; j++) {
+            int idx = (it & 1) ? j : n_noncontact - 1 - j;
+            x = solve_row(&rows[idx], dv);
+            if (x * x > res) res = x * x;
+        }
+        for (int c = 0; c < nc; c++) {
+            x = solve_row(&rows[normal_base + c], dv);
+            if (x * x > res) res = x * x;
+        }
+        for (int c = 0; c < nc; c++) {
+            orow *a = &rows[fric_base + 2 * c], *b = &rows[fric_base + 2 * c + 1];
+            x = solve_cone(a, b, rows[normal_base + c].lam, dv);
+            if (x * x > res) res = x * x;
+        }
+        if (res <= PM_SOLVER_RESIDUAL_THRESHOLD || it >= PM_SOLVER_ITERATIONS - 1) break;
+    }
+    if (stats) {
+        stats->substeps += 1;
+        stats->pgs_iterations += it + 1;
+        stats->rows += nr;
+        stats->contacts += nc;
+    }
+
+    /* integrate (btMultiBody::stepPositionsMultiDof) */
+    if (cfg->has_robot)
+        for (int d = 0; d < 9; d++) {
+            env->qd[d] = v1[d] + dv[d];
+            env->q[d] += dt * env->qd[d] + split_dq[d];
+        }
+    if (cfg->has_cube) {
+        for (int d = 0; d < 3; d++) {
+            env->comg[d] = v1[9 + d] + dv[9 + d];
+            env->cvel[d] = v1[12 + d] + dv[12 + d];
+            env->cpos[d] += dt * env->cvel[d];
+        }
+        double ang = v3_norm(env->comg), ax[3];
+        if (ang * dt > 0.5 * 1.5707963267948966) ang = 0.5 * 1.5707963267948966 / dt;
+        double f = ang < 0.001 ? (0.5 * dt - (dt * dt * dt) * 0.020833333333 * ang * ang) : sin(0.5 * ang * dt) / ang;
+        for (int d = 0; d < 3; d++) ax[d] = env->comg[d] * f;
+        double dq[4] = {ax[0], ax[1], ax[2], cos(0.5 * ang * dt)}, nq[4];
+        quat_mul(dq, env->cquat, nq);
+        double nn = sqrt(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
+        for (int d = 0; d < 4; d++) env->cquat[d] = nq[d] / nn;
+    }
+}
+
+void po_sim_step(const po_config *cfg, po_env *env, po_stats *stats) {
+    for (int s = 0; s < PM_SUBSTEPS; s++) po_substep(cfg, env, stats);
+}
+
+/* setJointMotorControlArray(POSITION_CONTROL) -> btMultiBodyJointMotor:
+ * kp 0.1, kd 1.0, target velocity 0, max impulse = force * 1/500
+ * (pybullet.py:462-477). */
+void po_control_joints(po_env *env, int n, const int32_t *joints, const double *targets, const double *forces) {
+    model_init();
+    for (int i = 0; i < n; i++) {
+        int d = -1;
+        for (int j = 0; j < 9; j++) if (dof_link[j] == joints[i]) d = j;
+        if (d < 0) continue;
+        env->m_target[d] = targets[i];
+        env->m_kp[d] = PM_MOTOR_KP;
+        env->m_kd[d] = PM_MOTOR_KD;
+        env->m_vel[d] = 0.0;
+        env->m_maximp[d] = forces[i] * PM_TIMESTEP;
+    }
+}
+
+/* getEulerFromQuaternion (pybullet.py:318-321) */
+void po_euler_from_quaternion(const double q[4], double rpy[3]) {
+    double sqx = q[0] * q[0], sqy = q[1] * q[1], sqz = q[2] * q[2], squ = q[3] * q[3];
+    double sarg = -2.0 * (q[0] * q[2] - q[3] * q[1]);
+    if (sarg <= -0.99999) {
+        rpy[0] = 0.0; rpy[1] = -0.5 * 3.14159265358979323846; rpy[2] = 2.0 * atan2(q[0], -q[1]);
+    } else if (sarg >= 0.99999) {
+        rpy[0] = 0.0; rpy[1] = 0.5 * 3.14159265358979323846; rpy[2] = 2.0 * atan2(-q[0], q[1]);
+    } else {
+        rpy[0] = atan2(2.0 * (q[1] * q[2] + q[3] * q[0]), squ - sqx - sqy + sqz);
+        rpy[1] = asin(sarg);
+        rpy[2] = atan2(2.0 * (q[0] * q[1] + q[3] * q[2]), squ + sqx - sqy - sqz);
+    }
+}
+
+/* ------------------------------------------------------------- numpy RNG */
+typedef unsigned __int128 u128;
+static const u128 PCG_MULT = (((u128)0x2360ED051FC65DA4ULL) << 64) | 0x4385DF649FCCF645ULL;
+
+static void pcg_load(const uint64_t rng[4], u128 *st, u128 *inc) {
+    *st = (((u128)rng[0]) << 64) | rng[1];
+    *inc = (((u128)rng[2]) << 64) | rng[3];
+}
+static void pcg_store(uint64_t rng[4], u128 st, u128 inc) {
+    rng[0] = (uint64_t)(st >> 64); rng[1] = (uint64_t)st;
+    rng[2] = (uint64_t)(inc >> 64); rng[3] = (uint64_t)inc;
+}
+
+/* numpy.random.SeedSequence(seed).generate_state(4, uint64) -> PCG64 seed
+ * (gymnasium.utils.seeding.np_random, called at core.py:244). */
+void po_pcg64_seed(uint64_t seed, uint64_t rng[4]) {
+    const uint32_t INIT_A = 0x43b0d7e5u, MULT_A = 0x931e8875u, INIT_B = 0x8b51f9ddu, MULT_B = 0x58f38dedu;
+    const uint32_t MIX_L = 0xca01f9ddu, MIX_R = 0x4973f715u;
+    uint32_t ent[2];
+    int nent = 1;
+    ent[0] = (uint32_t)seed;
+    if (seed >> 32) { ent[1] = (uint32_t)(seed >> 32); nent = 2; }
+    uint32_t pool[4], hc = INIT_A;
+#define HASHMIX(val, out)              \
+    {                                  \
+        uint32_t v_ = (val) ^ hc;      \
+        hc *= MULT_A;                  \
+        v_ *= hc;                      \
+        v_ ^= v_ >> 16;                \
+        out = v_;                      \
+    }
+    for (int i = 0; i < 4; i++) HASHMIX(i < nent ? ent[i] : 0u, pool[i]);
+    for (int s = 0; s < 4; s++)
+        for (int d = 0; d < 4; d++)
+            if (s != d) {
+                uint32_t hm;
+                HASHMIX(pool[s], hm);
+                uint32_t r = MIX_L * pool[d] - MIX_R * hm;
+                r ^= r >> 16;
+                pool[d] = r;
+            }
+#undef HASHMIX
+    uint32_t words[8], hb = INIT_B;
+    for (int i = 0; i < 8; i++) {
+        uint32_t v = pool[i % 4];
+        v ^= hb;
+        hb *= MULT_B;
+        v *= hb;
+        v ^= v >> 16;
+        words[i] = v;
+    }
+    uint64_t val[4];
+    for (int i = 0; i < 4; i++) val[i] = (uint64_t)words[2 * i] | ((uint64_t)words[2 * i + 1] << 32);
+    /* pcg64_set_seed: seed = (val[0] << 64 | val[1]), inc = (val[2] << 64 | val[3]) */
+    u128 initstate = (((u128)val[0]) << 64) | val[1];
+    u128 initseq = (((u128)val[2]) << 64) | val[3];
+    u128 st = 0, inc = (initseq << 1) | 1u;
+    st = st * PCG_MULT + inc;
+    st += initstate;
+    st = st * PCG_MULT + inc;
+    pcg_store(rng, st, inc);
+}
+
+uint64_t po_pcg64_next(uint64_t rng[4]) {
+    u128 st, inc;
+    pcg_load(rng, &st, &inc);
+    st = st * PCG_MULT + inc;
+    pcg_store(rng, st, inc);
+    uint64_t x = (uint64_t)(st >> 64) ^ (uint64_t)st;
+    unsigned rot = (unsigned)(st >> 122);
+    return (x >> rot) | (x << ((64 - rot) & 63));
+}
+
+double po_pcg64_double(uint64_t rng[4]) { return (double)(po_pcg64_next(rng) >> 11) * (1.0 / 9007199254740992.0); }
+
+/* Generator.uniform(low, high): low + (high - low) * next_double */
+static double uniform(uint64_t rng[4], double lo, double hi) {
+    double range = hi - lo;
+    double u = po_pcg64_double(rng);
+    return lo + range * u;
+}
+
+/* ------------------------------------------------------------- env layer */
+void po_default_config(po_config *cfg, int task, int control, int reward) {
+    memset(cfg, 0, sizeof *cfg);
+    cfg->task = task;
+    cfg->control = control;
+    cfg->reward = reward;
+    /* panda_tasks.py:46,62,78: Reach/Push block the gripper, PickAndPlace not */
+    cfg->block_gripper = task != PO_TASK_PICK_AND_PLACE;
+    cfg->has_table = cfg->has_plane = 1;
+    cfg->has_cube = task != PO_TASK_REACH;
+    cfg->has_robot = 1;
+    cfg->base[0] = PM_BASE_X;
+    cfg->cube_half = PM_CUBE_HALF;
+    cfg->cube_mass = PM_CUBE_MASS;
+}
+
+void po_init_env(const po_config *cfg, po_env *env) {
+    model_init();
+    (void)cfg;
+    memset(env, 0, sizeof *env);
+    env->cquat[3] = 1.0;
+    /* PhysicsServerCommandProcessor::createJointMotors: velocity motor,
+     * target 0, kd 1, max impulse 1 on every revolute/prismatic joint */
+    for (int d = 0; d < 9; d++) {
+        env->m_kd[d] = 1.0;
+        env->m_maximp[d] = PM_DEFAULT_MOTOR_MAX_IMPULSE;
+    }
+    po_pcg64_seed(0, env->rng);
+}
+
+int po_obs_dim(const po_config *cfg) {
+    int robot = cfg->block_gripper ? 6 : 7;
+    return robot + (cfg->task == PO_TASK_REACH ? 0 : 12);
+}
+
+int po_action_dim(const po_config *cfg) {
+    return (cfg->control == PO_CONTROL_EE ? 3 : 7) + (cfg->block_gripper ? 0 : 1);
+}
+
+/* utils.py:4-15 distance + is_success (reach.py:56-58, push.py:89-91):
+ * norm of (float32 achieved - float64 goal) in float64, d < 0.05 */
+static double goal_distance(const float ag[3], const double dg[3]) {
+    double d0 = (double)ag[0] - dg[0], d1 = (double)ag[1] - dg[1], d2 = (double)ag[2] - dg[2];
+    double s = d0 * d0;
+    s = s + d1 * d1;
+    s = s + d2 * d2;
+    return sqrt(s);
+}
+
+uint8_t po_is_success(const float ag[3], const double dg[3]) { return goal_distance(ag, dg) < PM_DISTANCE_THRESHOLD; }
+
+/* compute_reward (reach.py:60-65, push.py:93-98, pick_and_place.py:91-96) */
+float po_compute_reward(int reward_type, const float ag[3], const double dg[3]) {
+    double d = goal_distance(ag, dg);
+    if (reward_type == PO_REWARD_SPARSE) return d > PM_DISTANCE_THRESHOLD ? -1.0f : -0.0f;
+    return -(float)d;
+}
+
+/* RobotTaskEnv._get_obs (core.py:229-238) with Panda.get_obs (panda.py:109-119)
+ * and Push/PickAndPlace.get_obs (push.py:49-63) */
+void po_get_obs(const po_config *cfg, const po_env *env, float *obs, float *ag, float *dg) {
+    double p[3], qq[4], v[3], w[3];
+    po_link_state(cfg, env, PM_EE_LINK, p, qq, v, w);
+    int o = 0;
+    for (int d = 0; d < 3; d++) obs[o++] = (float)p[d];
+    for (int d = 0; d < 3; d++) obs[o++] = (float)v[d];
+    if (!cfg->block_gripper) obs[o++] = (float)(env->q[7] + env->q[8]);
+    if (cfg->task != PO_TASK_REACH) {
+        double e[3];
+        po_euler_from_quaternion(env->cquat, e);
+        for (int d = 0; d < 3; d++) obs[o++] = (float)env->cpos[d];
+        for (int d = 0; d < 3; d++) obs[o++] = (float)e[d];
+        for (int d = 0; d < 3; d++) obs[o++] = (float)env->cvel[d];
+        for (int d = 0; d < 3; d++) obs[o++] = (float)env->comg[d];
+        for (int d = 0; d < 3; d++) ag[d] = (float)env->cpos[d];
+    } else {
+        for (int d = 0; d < 3; d++) ag[d] = (float)p[d];
+    }
+    for (int d = 0; d < 3; d++) dg[d] = (float)env->goal[d];
+}
+
+/* RobotTaskEnv.reset (core.py:240-250): new Generator(PCG64(SeedSequence(seed)))
+ * when a seed is given; Panda.reset -> neutral joints with zero velocity
+ * (panda.py:121-126); Task.reset draws the goal then the object
+ * (reach.py:47-54, push.py:69-87, pick_and_place.py:65-85).  The object's
+ * velocity is not reset (only resetBasePositionAndOrientation is called). */
+void po_reset(const po_config *cfg, po_env *env, int has_seed, uint64_t seed, float *obs, float *ag, float *dg) {
+    model_init();
+    if (has_seed) po_pcg64_seed(seed, env->rng);
+    static const double neutral[9] = PM_NEUTRAL_Q;
+    for (int d = 0; d < 9; d++) { env->q[d] = neutral[d]; env->qd[d] = 0.0; }
+    if (cfg->task == PO_TASK_REACH) {
+        env->goal[0] = uniform(env->rng, -0.15, 0.15);
+        env->goal[1] = uniform(env->rng, -0.15, 0.15);
+        env->goal[2] = uniform(env->rng, 0.0, 0.3);
+    } else {
+        double zr = cfg->task == PO_TASK_PICK_AND_PLACE ? 0.2 : 0.0;
+        double n0 = uniform(env->rng, -0.15, 0.15), n1 = uniform(env->rng, -0.15, 0.15), n2 = uniform(env->rng, 0.0, zr);
+        if (cfg->task == PO_TASK_PICK_AND_PLACE && po_pcg64_double(env->rng) < 0.3) n2 = 0.0;
+        env->goal[0] = 0.0 + n0;
+        env->goal[1] = 0.0 + n1;
+        env->goal[2] = cfg->cube_half + n2;
+        double o0 = uniform(env->rng, -0.15, 0.15), o1 = uniform(env->rng, -0.15, 0.15), o2 = uniform(env->rng, 0.0, 0.0);
+        env->cpos[0] = 0.0 + o0;
+        env->cpos[1] = 0.0 + o1;
+        env->cpos[2] = cfg->cube_half + o2;
+        env->cquat[0] = env->cquat[1] = env->cquat[2] = 0.0;
+        env->cquat[3] = 1.0;
+    }
+    env->elapsed = 0;
+    if (obs) po_get_obs(cfg, env, obs, ag, dg);
+}
+
+/* Panda.set_action (panda.py:52-107) */
+static void set_action(const po_config *cfg, po_env *env, const float *action) {
+    int na = po_action_dim(cfg);
+    float a[8];
+    for (int i = 0; i < na; i++) a[i] = action[i] < -1.0f ? -1.0f : (action[i] > 1.0f ? 1.0f : action[i]);
+    double target[9];
+    if (cfg->control == PO_CONTROL_EE) {
+        double p[3], qq[4], v[3], w[3];
+        po_link_state(cfg, env, PM_EE_LINK, p, qq, v, w);
+        double tp[3];
+        for (int d = 0; d < 3; d++) tp[d] = p[d] + (double)(a[d] * 0.05f);
+        if (tp[2] < 0.0) tp[2] = 0.0;
+        static const double orn[4] = {1.0, 0.0, 0.0, 0.0};
+        double qik[9];
+        po_inverse_kinematics(cfg, env->q, PM_EE_LINK, tp, orn, qik);
+        for (int d = 0; d < 7; d++) target[d] = qik[d];
+    } else {
+        for (int d = 0; d < 7; d++) target[d] = env->q[d] + (double)(a[d] * 0.05f);
+    }
+    double width = 0.0;
+    if (!cfg->block_gripper) width = (env->q[7] + env->q[8]) + (double)(a[na - 1] * 0.2f);
+    target[7] = target[8] = width / 2.0;
+    static const int32_t joints[9] = {0, 1, 2, 3, 4, 5, 6, 9, 10};
+    static const double forces[9] = PM_JOINT_FORCES;
+    po_control_joints(env, 9, joints, target, forces);
+}
+
+/* RobotTaskEnv.step (core.py:280-289) + TimeLimit(50) (__init__.py:18-40) */
+void po_step(const po_config *cfg, po_env *env, const float *action, float *obs, float *ag, float *dg,
+             float *reward, uint8_t *terminated, uint8_t *truncated, int autoreset, float *final_obs,
+             float *final_ag, po_stats *stats) {
+    model_init();
+    set_action(cfg, env, action);
+    po_sim_step(cfg, env, stats);
+    po_get_obs(cfg, env, obs, ag, dg);
+    *terminated = po_is_success(ag, env->goal);
+    *reward = po_compute_reward(cfg->reward, ag, env->goal);
+    env->elapsed += 1;
+    *truncated = env->elapsed >= PM_MAX_EPISODE_STEPS;
+    if (autoreset && (*terminated || *truncated)) {
+        int od = po_obs_dim(cfg);
+        if (final_obs) memcpy(final_obs, obs, sizeof(float) * od);
+        if (final_ag) memcpy(final_ag, ag, sizeof(float) * 3);
+        po_reset(cfg, env, 0, 0, obs, ag, dg);
+    }
+}
+
+void po_step_batch(const po_config *cfg, po_env *envs, int n, const float *actions, float *obs, float *ag,
+                   float *dg, float *reward, uint8_t *terminated, uint8_t *truncated, int autoreset,
+                   po_stats *stats) {
+    int na = po_action_dim(cfg), od = po_obs_dim(cfg);
+    for (int i = 0; i < n; i++)
+        po_step(cfg, &envs[i], actions + (size_t)i * na, obs + (size_t)i * od, ag + (size_t)i * 3,
+                dg + (size_t)i * 3, reward + i, terminated + i, truncated + i, autoreset, NULL, NULL, stats);
+}

@@ -1,0 +1,94 @@
+/*
+ * panda_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU fp64 restatement of the PandaReach/Push/PickAndPlace-v3 step()/reset()
+ * path of the reference (panda_gym/envs/core.py:240-289, robots/panda.py,
+ * tasks/{reach,push,pick_and_place}.py, pybullet.py) and of the subset of the
+ * third-party PyBullet 3.2.5 engine those files call (pinned version:
+ * env.yml:107; not vendored in /root/reference, so its published algorithm is
+ * restated: btMultiBody forward dynamics, btMultiBodyJointMotor,
+ * btMultiBodyJointLimitConstraint, btMultiBodyConstraintSolver PGS,
+ * IKTrajectoryHelper DLS inverse kinematics, getEulerFromQuaternion) and of
+ * numpy's SeedSequence/PCG64/Generator.uniform used by gymnasium.seeding.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+ * this library, and only as the checker.  The product path
+ * (panda-lang-manip_amd/) never links or calls it.
+ *
+ * Parity pins: tests/golden/ (task layer, generated from the reference's own
+ * task classes) and the known-answer tests of test/pybullet_test.py.
+ */
+#ifndef PANDA_ORACLE_H
+#define PANDA_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { PO_TASK_REACH = 0, PO_TASK_PUSH = 1, PO_TASK_PICK_AND_PLACE = 2 };
+enum { PO_CONTROL_EE = 0, PO_CONTROL_JOINTS = 1 };
+enum { PO_REWARD_SPARSE = 0, PO_REWARD_DENSE = 1 };
+
+typedef struct {
+    int32_t task, control, reward, block_gripper;
+    int32_t has_table, has_plane, has_cube, has_robot;
+    double base[3];
+    double cube_half, cube_mass;
+} po_config;
+
+typedef struct {
+    double q[9], qd[9];
+    double m_target[9], m_kp[9], m_kd[9], m_vel[9], m_maximp[9];
+    double cpos[3], cquat[4], cvel[3], comg[3]; /* cube: quat (x,y,z,w) base->world */
+    double goal[3];
+    int64_t elapsed;
+    uint64_t rng[4]; /* PCG64 state hi, lo, inc hi, lo */
+} po_env;
+
+typedef struct {
+    int64_t substeps, pgs_iterations, rows, contacts;
+} po_stats;
+
+void po_default_config(po_config *cfg, int task, int control, int reward);
+void po_init_env(const po_config *cfg, po_env *env);
+
+/* --- engine-level primitives (pybullet.py wrapper semantics) --- */
+void po_link_state(const po_config *cfg, const po_env *env, int link, double pos[3], double quat[4],
+                   double lin_vel[3], double ang_vel[3]);
+void po_inverse_kinematics(const po_config *cfg, const double q_start[9], int link, const double pos[3],
+                           const double orn[4], double q_out[9]);
+void po_control_joints(po_env *env, int n, const int32_t *joints, const double *targets, const double *forces);
+void po_substep(const po_config *cfg, po_env *env, po_stats *stats);
+void po_sim_step(const po_config *cfg, po_env *env, po_stats *stats);
+void po_euler_from_quaternion(const double q[4], double rpy[3]);
+
+/* --- env-level (core.py) --- */
+int po_obs_dim(const po_config *cfg);
+int po_action_dim(const po_config *cfg);
+void po_reset(const po_config *cfg, po_env *env, int has_seed, uint64_t seed, float *obs, float *ag, float *dg);
+void po_get_obs(const po_config *cfg, const po_env *env, float *obs, float *ag, float *dg);
+void po_step(const po_config *cfg, po_env *env, const float *action, float *obs, float *ag, float *dg,
+             float *reward, uint8_t *terminated, uint8_t *truncated, int autoreset, float *final_obs,
+             float *final_ag, po_stats *stats);
+void po_step_batch(const po_config *cfg, po_env *envs, int n, const float *actions, float *obs, float *ag,
+                   float *dg, float *reward, uint8_t *terminated, uint8_t *truncated, int autoreset,
+                   po_stats *stats);
+float po_compute_reward(int reward_type, const float ag[3], const double dg[3]);
+uint8_t po_is_success(const float ag[3], const double dg[3]);
+
+/* --- numpy SeedSequence / PCG64 --- */
+void po_pcg64_seed(uint64_t seed, uint64_t rng[4]);
+uint64_t po_pcg64_next(uint64_t rng[4]);
+double po_pcg64_double(uint64_t rng[4]);
+
+/* --- introspection used by the tests --- */
+void po_mass_matrix(const po_config *cfg, const double q[9], double M[81]);
+void po_bias_forces(const po_config *cfg, const double q[9], const double qd[9], double h[9]);
+void po_link_inertia(int link, double inertia[3]);
+void po_set_link_aabb(int link, double lx, double ly, double lz);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,193 @@
+"""CPU tests: pin the oracle (fp64 CPU restatement) before trusting it.
+
+* Physics known-answer tests transcribed from the reference's own suite,
+  /root/reference/test/pybullet_test.py (atol 1e-3 as there).
+* Task-layer golden vectors generated from the reference's task classes
+  (tests/golden/make_golden.py): bit-exact.
+* numpy SeedSequence/PCG64 restatement vs numpy itself: bit-exact.
+* seed_test.py / save_and_restore_test.py behaviours.
+"""
+import copy
+
+import numpy as np
+import oracle as O
+import pytest
+
+
+def kat_config():
+    # PyBullet() + loadURDF("franka_panda/panda.urdf", basePosition=0, useFixedBase=True), no other bodies
+    return O.config("reach", base=(0.0, 0.0, 0.0), has_table=0, has_plane=0, has_cube=0)
+
+
+def test_dt():  # pybullet_test.py:30-35
+    assert O.lib() is not None
+    assert abs(20 * (1.0 / 500) - 0.04) < 1e-12
+
+
+def test_get_link_position():  # pybullet_test.py:124-136
+    cfg = kat_config()
+    env = O.new_env(cfg)
+    pos, *_ = O.link_state(cfg, env, 1)
+    assert np.allclose(pos, [0.000, 0.060, 0.373], atol=1e-3)
+
+
+@pytest.fixture(scope="module")
+def joint5_after_step():  # pybullet_test.py:139-204: control_joints([5],[0.3],[5.0]) + step()
+    cfg = kat_config()
+    env = O.new_env(cfg)
+    O.control_joints(env, [5], [0.3], [5.0])
+    O.sim_step(cfg, env)
+    return cfg, env
+
+
+def test_get_link_orientation(joint5_after_step):  # :139-153
+    cfg, env = joint5_after_step
+    _, orn, _, _ = O.link_state(cfg, env, 5)
+    assert np.allclose(orn, [0.707, -0.02, 0.02, 0.707], atol=1e-3)
+
+
+def test_get_link_velocity(joint5_after_step):  # :156-170
+    cfg, env = joint5_after_step
+    _, _, v, _ = O.link_state(cfg, env, 5)
+    assert np.allclose(v, [-0.0068, 0.0000, 0.1186], atol=1e-3)
+
+
+def test_get_link_angular_velocity(joint5_after_step):  # :173-187
+    cfg, env = joint5_after_step
+    _, _, _, w = O.link_state(cfg, env, 5)
+    assert np.allclose(w, [0.000, -2.969, 0.000], atol=1e-3)
+
+
+def test_get_joint_angle(joint5_after_step):  # :190-204
+    _, env = joint5_after_step
+    assert np.allclose(env.q[5], 0.063, atol=1e-3)
+
+
+def test_inverse_kinematics():  # pybullet_test.py:254-266
+    cfg = kat_config()
+    q = O.inverse_kinematics(cfg, np.zeros(9), 6, [0.4, 0.5, 0.6], [0.707, -0.02, 0.02, 0.707])
+    assert np.allclose(q, [1.000, 1.223, -1.113, -0.021, -0.917, 0.666, -0.499, 0.0, 0.0], atol=1e-3)
+
+
+def test_box_free_fall_velocity():  # pybullet_test.py:56-64 (1 kg box, half extents 0.5, one step())
+    cfg = O.config("push", base=(0, 0, 0), has_table=0, has_plane=0, has_robot=0, cube_half=0.5, cube_mass=1.0)
+    env = O.new_env(cfg)
+    O.sim_step(cfg, env)
+    assert np.allclose(np.array(env.cvel), [0.0, 0.0, -0.392], atol=1e-3)
+    assert np.allclose(np.array(env.comg), 0.0, atol=1e-3)  # :89-97
+    e = np.zeros(3)
+    O.lib().po_euler_from_quaternion(np.array(env.cquat).ctypes.data_as(O.C.POINTER(O.C.c_double)),
+                                     e.ctypes.data_as(O.C.POINTER(O.C.c_double)))
+    assert np.allclose(e, 0.0, atol=1e-3)  # :78-86
+    assert np.allclose(np.array(env.cquat), [0, 0, 0, 1], atol=1e-3)  # :67-75
+
+
+def test_set_joint_angles_roundtrip():  # pybullet_test.py:221-251
+    cfg = kat_config()
+    env = O.new_env(cfg)
+    env.q[3], env.q[4] = 0.4, 0.5
+    assert env.q[3] == 0.4 and env.q[4] == 0.5
+
+
+def test_euler_from_quaternion_branches():
+    for q in ([0, 0, 0, 1], [0.707, -0.02, 0.02, 0.707], [0, 0.7071068, 0, 0.7071068], [0, -0.7071068, 0, 0.7071068]):
+        q = np.array(q, float) / np.linalg.norm(q)
+        e = np.zeros(3)
+        O.lib().po_euler_from_quaternion(q.ctypes.data_as(O.C.POINTER(O.C.c_double)),
+                                         e.ctypes.data_as(O.C.POINTER(O.C.c_double)))
+        # reconstruct (XYZ fixed axes: R = Rz(yaw) Ry(pitch) Rx(roll))
+        h = e / 2  # btQuaternion::setEulerZYX (getQuaternionFromEuler)
+        cr, sr, cp, sp, cy, sy = np.cos(h[0]), np.sin(h[0]), np.cos(h[1]), np.sin(h[1]), np.cos(h[2]), np.sin(h[2])
+        w = cr * cp * cy + sr * sp * sy
+        x = sr * cp * cy - cr * sp * sy
+        y = cr * sp * cy + sr * cp * sy
+        z = cr * cp * sy - sr * sp * cy
+        r = np.array([x, y, z, w])
+        assert min(np.abs(r - q).max(), np.abs(r + q).max()) < 1e-4
+
+
+def test_neutral_pose_observation():
+    # Panda.reset -> neutral joints (panda.py:121-126); ee = grasptarget COM
+    cfg = O.config("reach")
+    env = O.new_env(cfg)
+    obs, ag, dg = O.reset(cfg, env, seed=0)
+    assert np.allclose(obs[:3], [0.0384397, 0.0, 0.1974001], atol=1e-6)
+    assert np.all(obs[3:6] == 0.0)
+    assert np.array_equal(ag, obs[:3])
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2**32 - 1, 2**32, 2**63 + 7, 2**64 - 1])
+def test_pcg64_matches_numpy(seed):
+    st = O.pcg64_seed(seed)
+    bg = np.random.PCG64(np.random.SeedSequence(seed))
+    assert [O.pcg64_next(st) for _ in range(16)] == [int(bg.random_raw()) for _ in range(16)]
+
+
+@pytest.mark.parametrize("task", ["reach", "push", "pick_and_place"])
+def test_goal_sampling_golden(task, golden):
+    cfg = O.config(task)
+    for i, s in enumerate(golden["seeds"]):
+        env = O.new_env(cfg)
+        for r in range(golden[f"{task}_goal"].shape[1]):
+            O.reset(cfg, env, seed=int(s) if r == 0 else None)
+            assert np.array_equal(np.array(env.goal), golden[f"{task}_goal"][i, r])
+            if task != "reach":
+                assert np.array_equal(np.array(env.cpos), golden[f"{task}_object"][i, r])
+
+
+def test_reward_and_success_golden(golden):
+    ag, dg = golden["reward_ag"], golden["reward_dg"]
+    sp = np.array([O.compute_reward("sparse", a, d) for a, d in zip(ag, dg)], np.float32)
+    de = np.array([O.compute_reward("dense", a, d) for a, d in zip(ag, dg)], np.float32)
+    su = np.array([O.is_success(a, d) for a, d in zip(ag, dg)])
+    assert np.array_equal(sp.view(np.uint32), golden["reward_sparse"].view(np.uint32))
+    assert np.array_equal(de.view(np.uint32), golden["reward_dense"].view(np.uint32))
+    assert np.array_equal(su, golden["success"])
+
+
+def _rollout(task, seed, actions, control="ee"):
+    cfg = O.config(task, control=control)
+    env = O.new_env(cfg)
+    O.reset(cfg, env, seed=seed)
+    out = None
+    for a in actions:
+        out = O.step(cfg, env, np.asarray(a, np.float32), autoreset=True)
+    return out
+
+
+@pytest.mark.parametrize("task,seed,na", [("reach", 12345, 3), ("push", 6789, 3), ("pick_and_place", 794512, 4)])
+def test_seed_determinism(task, seed, na):  # seed_test.py:7-122
+    actions = np.random.default_rng(seed).uniform(-1, 1, size=(6, na))
+    a = _rollout(task, seed, actions)
+    b = _rollout(task, seed, actions)
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(x, y)
+
+
+def test_save_and_restore_bit_equal():  # save_and_restore_test.py:9-27
+    cfg = O.config("reach")
+    env = O.new_env(cfg)
+    O.reset(cfg, env, seed=3)
+    saved = copy.deepcopy(env)
+    action = np.array([0.3, -0.2, 0.5], np.float32)
+    o1 = O.step(cfg, env, action)
+    O.reset(cfg, env, seed=99)
+    env = copy.deepcopy(saved)
+    o2 = O.step(cfg, env, action)
+    for x, y in zip(o1[:3], o2[:3]):
+        assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("task", ["reach", "push", "pick_and_place"])
+def test_random_rollout_is_finite_and_bounded(task):  # envs_test.py:6-14 (shortened)
+    cfg = O.config(task)
+    env = O.new_env(cfg)
+    O.reset(cfg, env, seed=1)
+    rng = np.random.default_rng(0)
+    na = O.action_dim(cfg)
+    resets = 0
+    for _ in range(120):
+        obs, ag, dg, r, te, tr = O.step(cfg, env, rng.uniform(-1, 1, na).astype(np.float32), autoreset=True)
+        assert np.all(np.isfinite(obs)) and np.all(np.abs(obs) < 10.0)
+        resets += te or tr
+    assert resets >= 2  # TimeLimit(50) fired
