@@ -1,0 +1,185 @@
+#!/usr/bin/env python
+"""Benchmark: batched env-steps/s of PandaPush-v3 on MI355X (BASELINE.json metric).
+
+Workload: PandaPush-v3 (sparse, ee control), 65 536
+envs per GPU (weak scaling; 524 288 at 8 GPUs), env i of rank r seeded with
+12345 + r*B + i, i.i.d. U(-1, 1) fp32 actions from a Philox stream seeded
+0xC0FFEE + rank, auto-reset on terminated|truncated.  One "step" = one fused
+RobotTaskEnv.step() of every env (20 physics substeps + IK + obs + reward).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one process per GPU, RCCL).  Rank 0 prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "panda-lang-manip_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_PEAK_TFLOPS = 157.3
+
+
+def algorithmic_bytes_per_env_step(obs_dim: int, action_dim: int) -> int:
+    """Bytes one env-step must move through HBM:
+    read q,qd (18 f32), object 13 f32, goal 3 f64, TimeLimit counter, action;
+    write q,qd, 45 motor f32, object, counter, obs, ag, dg, reward, 2 flags,
+    final_obs + final_ag."""
+    read = 18 * 4 + 13 * 4 + 3 * 8 + 4 + action_dim * 4
+    write = 18 * 4 + 45 * 4 + 13 * 4 + 4 + obs_dim * 4 + 12 + 12 + 4 + 2 + obs_dim * 4 + 12
+    return read + write
+
+
+def cpu_baseline(task: str, seconds: float):
+    """The oracle (fp64 C restatement, 1 thread) on a bounded sample of the same workload."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    cfg = O.config(task)
+    n_env = 64
+    envs = (O.Env * n_env)()
+    for i in range(n_env):
+        O.lib().po_init_env(O.C.byref(cfg), O.C.byref(envs[i]))
+        O.lib().po_reset(O.C.byref(cfg), O.C.byref(envs[i]), 1, 12345 + i, None, None, None)
+    na, od = O.action_dim(cfg), O.obs_dim(cfg)
+    rng = np.random.default_rng(0xC0FFEE)
+    obs = np.zeros((n_env, od), np.float32)
+    ag = np.zeros((n_env, 3), np.float32)
+    dg = np.zeros((n_env, 3), np.float32)
+    rew = np.zeros(n_env, np.float32)
+    te = np.zeros(n_env, np.uint8)
+    tr = np.zeros(n_env, np.uint8)
+    fp = lambda a: a.ctypes.data_as(O.C.POINTER(O.C.c_float))
+    u8 = lambda a: a.ctypes.data_as(O.C.POINTER(O.C.c_uint8))
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        a = rng.uniform(-1, 1, size=(n_env, na)).astype(np.float32)
+        O.lib().po_step_batch(O.C.byref(cfg), envs, n_env, fp(a), fp(obs), fp(ag), fp(dg), fp(rew), u8(te), u8(tr), 1,
+                              None)
+        steps += 1
+    dt = time.perf_counter() - t0
+    return {"value": round(n_env * steps / dt, 2), "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{n_env} envs x {steps} steps of PandaPush-v3 in {dt:.1f} s on 1 host thread "
+                      f"(fp64 oracle; PyBullet not installed)"}
+
+
+def load_pmc_traffic(workload: str):
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        data = json.load(open(path))
+        return data.get(workload)
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--env-id", default="PandaPush-v3")
+    ap.add_argument("--batch", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import pandasim
+    from pandasim.envs import REGISTRY
+
+    B = args.batch
+    env = pandasim.make(args.env_id, num_envs=B, device=dev)
+    spec = REGISTRY[args.env_id]
+    seeds = 12345 + rank * B
+    env.reset(seed=seeds)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0xC0FFEE + rank)
+    n_act = args.warmup + args.steps
+    actions = torch.rand(n_act, B, env.action_dim, device=dev, generator=gen) * 2 - 1
+    returns = torch.zeros(B, device=dev)
+
+    for k in range(args.warmup):
+        env.step(actions[k], copy=False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    stops = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        a = actions[args.warmup + k]
+        starts[k].record()
+        obs, r, te, tr, info = env.step(a, copy=False)
+        stops[k].record()
+        returns.add_(r)
+    if world > 1:
+        gathered = [torch.empty_like(returns) for _ in range(world)] if rank == 0 else None
+        dist.gather(returns, gathered, dst=0)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = sum(s.elapsed_time(e) for s, e in zip(starts, stops)) / args.steps
+    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    total_env_steps = world * B * args.steps
+    value = total_env_steps / elapsed
+    bytes_env = algorithmic_bytes_per_env_step(env.obs_dim, env.action_dim)
+    achieved = bytes_env * B / (kernel_ms * 1e-3) / 1e9
+    workload = f"{args.env_id} x{B}/gpu"
+    out = {
+        "metric": "env steps/sec (batched) PandaPush-v3 at 1/2/4/8 MI355X vs PyBullet CPU",
+        "value": round(value, 1),
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded resets, U(-1,1) actions)",
+        "config": {"workload": workload, "env_id": args.env_id, "task": spec["task"],
+                   "control": spec["control_type"], "reward": spec["reward_type"], "batch_per_gpu": B,
+                   "global_batch": world * B, "substeps": 20, "parallelism": f"batch shard x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": load_pmc_traffic(workload),
+                     "kernel": "k_step<PUSH,EE>", "kernel_ms": round(kernel_ms, 4),
+                     "bytes_per_env_step": bytes_env},
+    }
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(spec["task"], args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

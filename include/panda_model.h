@@ -143,6 +143,8 @@
 #define PM_DEFAULT_FRICTION 0.5
 #define PM_CONTACT_MARGIN_GROUND 0.01
 #define PM_CONTACT_MARGIN_SPHERE 0.005
+#define PM_MAX_GROUND_CONTACTS 4
+#define PM_MAX_ROBOT_CONTACTS 4
 
 /* Task constants (tasks/reach.py:10-25, push.py:10-27, pick_and_place.py:11-29) */
 #define PM_DISTANCE_THRESHOLD 0.05

@@ -1,0 +1,137 @@
+/*
+ * pandasim.h — C ABI of the MI355X-native batched Panda simulator
+ * (libpandasim.so, built from panda-lang-manip_amd/csrc/pandasim.hip).
+ *
+ * Drop-in boundary for the reference's step()/reset() path.  Each entry point
+ * replaces one call site of /root/reference (cited per function); see
+ * INTEGRATION.md for the host-side binding (ctypes) a maintainer adds.
+ *
+ * Conventions
+ *   - Every buffer argument is a DEVICE pointer owned by the caller (PyTorch
+ *     tensors in panda-lang-manip_amd/pandasim); the library never allocates
+ *     per call and holds no host-language objects.
+ *   - Calls are asynchronous on the given HIP stream (hipStream_t passed as
+ *     void*; NULL = default stream).  One ps_ctx per (process, device); a
+ *     context is not re-entrant.
+ *   - Every call returns PS_OK (0) or a negative PS_ERR_* code; no C++
+ *     exception crosses the ABI.  ps_last_error() gives the message.
+ *   - Batched state lives in one caller-owned device buffer of
+ *     ps_layout.total_bytes bytes, structure-of-arrays, described by ps_layout.
+ *     save_state/restore_state (core.py:252-278) are copies of that buffer.
+ */
+#ifndef PANDASIM_H
+#define PANDASIM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PS_ABI_VERSION 1
+
+enum { PS_TASK_REACH = 0, PS_TASK_PUSH = 1, PS_TASK_PICK_AND_PLACE = 2 };
+enum { PS_CONTROL_EE = 0, PS_CONTROL_JOINTS = 1 };
+enum { PS_REWARD_SPARSE = 0, PS_REWARD_DENSE = 1 };
+enum { PS_OK = 0, PS_ERR_ARG = -1, PS_ERR_HIP = -2, PS_ERR_UNSUPPORTED = -3 };
+
+/* Scene/env configuration.  ps_default_config() fills the registered env
+ * (panda_gym/__init__.py:8-54 + envs/panda_tasks.py:31-79); the scene flags
+ * let tests build the reference's engine-level KAT scenes
+ * (test/pybullet_test.py). */
+typedef struct {
+    int32_t task, control, reward, block_gripper;
+    int32_t has_table, has_plane, has_cube, reserved;
+    float base[3];
+    float cube_half, cube_mass;
+} ps_config;
+
+/* State layout: byte offsets from the state pointer.  Float fields are rows
+ * of `stride` floats (env i at [row*stride + i]); goal is 3 rows of doubles,
+ * rng is 4 rows of uint64 (PCG64 state hi, lo, inc hi, lo), elapsed one row
+ * of int32 (TimeLimit counter). */
+enum {
+    PS_F_Q = 0,        /* 9 joint positions (DoF order: joints 0..6, 9, 10) */
+    PS_F_QD = 9,       /* 9 joint velocities */
+    PS_F_MTARGET = 18, /* 9 motor target positions */
+    PS_F_MKP = 27,     /* 9 motor position gains */
+    PS_F_MKD = 36,     /* 9 motor velocity gains */
+    PS_F_MVEL = 45,    /* 9 motor target velocities */
+    PS_F_MIMP = 54,    /* 9 motor max impulses (force * 1/500 s) */
+    PS_F_CPOS = 63,    /* 3 object position (world) */
+    PS_F_CQUAT = 66,   /* 4 object orientation quaternion x,y,z,w */
+    PS_F_CVEL = 70,    /* 3 object linear velocity */
+    PS_F_COMG = 73,    /* 3 object angular velocity */
+    PS_NUM_FLOAT_ROWS = 76
+};
+
+typedef struct {
+    int64_t num_envs, stride;
+    int64_t float_offset, goal_offset, rng_offset, elapsed_offset;
+    int64_t total_bytes;
+} ps_layout;
+
+typedef struct ps_ctx ps_ctx;
+
+int ps_abi_version(void);
+int ps_default_config(int task, int control, int reward, ps_config *out);
+int ps_state_layout(int64_t num_envs, ps_layout *out);
+
+/* gym.make(id) -> RobotTaskEnv.__init__ (core.py:209-227), minus the initial
+ * reset, which the caller issues with ps_reset. */
+int ps_create(const ps_config *cfg, int64_t num_envs, int device, ps_ctx **out);
+void ps_destroy(ps_ctx *ctx);
+const char *ps_last_error(const ps_ctx *ctx);
+int ps_obs_dim(const ps_ctx *ctx);
+int ps_action_dim(const ps_ctx *ctx);
+
+/* Zero state, identity object orientation and PyBullet's default joint
+ * velocity motors (loadURDF, core.py:40-52). */
+int ps_init_state(ps_ctx *ctx, void *state, void *stream);
+
+/* RobotTaskEnv.reset(seed) (core.py:240-250) for every env with mask[i] != 0
+ * (mask == NULL: all).  seeds != NULL: env i is re-seeded with
+ * Generator(PCG64(SeedSequence(seeds[i]))) (core.py:244); seeds == NULL: the
+ * env's current generator continues.  obs/ag/dg may be NULL. */
+int ps_reset(ps_ctx *ctx, void *state, const uint8_t *mask, const uint64_t *seeds, float *obs, float *ag,
+             float *dg, void *stream);
+
+/* RobotTaskEnv.step(action) (core.py:280-289) + TimeLimit(50), fused:
+ * Panda.set_action (panda.py:52-107, incl. calculateInverseKinematics) ->
+ * PyBullet.step (pybullet.py:52-55, 20 substeps) -> _get_obs -> is_success /
+ * compute_reward.  actions: [B, action_dim] f32.  obs [B, obs_dim], ag/dg
+ * [B,3], reward [B] f32, terminated/truncated [B] u8.  autoreset != 0:
+ * finished envs are reset in-kernel (generator continues) and obs/ag/dg hold
+ * the reset observation; final_obs/final_ag (may be NULL) receive the
+ * pre-reset observation of every env. */
+int ps_step(ps_ctx *ctx, void *state, const float *actions, float *obs, float *ag, float *dg, float *reward,
+            uint8_t *terminated, uint8_t *truncated, int autoreset, float *final_obs, float *final_ag,
+            void *stream);
+
+/* Engine level: PyBullet.step() (pybullet.py:52-55) with the motors already in
+ * the state (n_substeps of 1/500 s). */
+int ps_sim_step(ps_ctx *ctx, void *state, int n_substeps, void *stream);
+
+/* getLinkState(computeLinkVelocity=1) (pybullet.py:351-400) for all envs:
+ * pos/lin_vel/ang_vel [B,3], quat [B,4]; any output may be NULL. */
+int ps_link_state(ps_ctx *ctx, const void *state, int link, float *pos, float *quat, float *lin_vel,
+                  float *ang_vel, void *stream);
+
+/* calculateInverseKinematics (pybullet.py:479-497) from the current joint
+ * positions: pos [B,3] world, orn [B,4] (x,y,z,w), q_out [B,9]. */
+int ps_inverse_kinematics(ps_ctx *ctx, const void *state, int link, const float *pos, const float *orn,
+                          float *q_out, void *stream);
+
+/* Task.compute_reward / is_success (reach.py:56-65, push.py:89-98),
+ * vectorised for HER (core.py:226): n goal pairs [n,3], each f64 when its
+ * *_is_double flag is set, else f32.  As numpy does, the distance is computed
+ * in f64 when either side is f64 and in f32 (threshold 0.05f) when both are
+ * f32.  reward and success may be NULL. */
+int ps_compute_reward(int reward_type, const void *ag, int ag_is_double, const void *dg, int dg_is_double,
+                      float *reward, uint8_t *success, int64_t n, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -532,10 +532,12 @@ static int ground_top(const po_config *cfg, double x, double y, double *top) {
 }
 
 /* Contact generation (replaces Bullet's broadphase + box-box / convex
- * narrowphase with the proxies of panda_model.h), fixed order:
- *   1. gripper spheres vs cube (closest point on the cube)
- *   2. cube vertices vs ground (table top or plane), first 4 in vertex order
- *   3. gripper spheres vs ground */
+ * narrowphase with the proxies of panda_model.h), fixed order and caps:
+ *   1. cube vertices vs ground (table top or plane): the first
+ *      PM_MAX_GROUND_CONTACTS vertices (index order) within the margin
+ *   2. gripper spheres vs cube (closest point on the cube)
+ *   3. gripper spheres vs ground
+ *   2+3 share PM_MAX_ROBOT_CONTACTS slots, filled in that order. */
 static int gen_contacts(const po_config *cfg, const po_env *env, const okin *k, ocontact *out) {
     int nc = 0;
     double Rc[9];
@@ -547,9 +549,33 @@ static int gen_contacts(const po_config *cfg, const po_env *env, const okin *k, 
             m3_vec(k->R[SPH[s].link], SPH[s].c, t);
             for (int d = 0; d < 3; d++) sc[s][d] = k->o[SPH[s].link][d] + t[d];
         }
+    if (cfg->has_cube) {
+        double h = cfg->cube_half;
+        int ng = 0;
+        for (int v = 0; v < 8 && ng < PM_MAX_GROUND_CONTACTS; v++) {
+            double loc[3] = {(v & 1) ? h : -h, (v & 2) ? h : -h, (v & 4) ? h : -h}, pw[3];
+            m3_vec(Rc, loc, pw);
+            for (int d = 0; d < 3; d++) pw[d] += env->cpos[d];
+            double top;
+            if (!ground_top(cfg, pw[0], pw[1], &top)) continue;
+            double dist = pw[2] - top;
+            if (dist < PM_CONTACT_MARGIN_GROUND) {
+                ocontact *c = &out[nc++];
+                ng++;
+                c->bodyA = -2;
+                c->bodyB = -1;
+                c->n[0] = 0; c->n[1] = 0; c->n[2] = 1;
+                memcpy(c->pA, pw, sizeof pw);
+                c->pB[0] = pw[0]; c->pB[1] = pw[1]; c->pB[2] = top;
+                c->dist = dist;
+                c->mu = PM_DEFAULT_FRICTION * PM_DEFAULT_FRICTION;
+            }
+        }
+    }
+    int nr = 0;
     if (cfg->has_cube && cfg->has_robot) {
         double h = cfg->cube_half;
-        for (int s = 0; s < PM_NUM_SPHERES; s++) {
+        for (int s = 0; s < PM_NUM_SPHERES && nr < PM_MAX_ROBOT_CONTACTS; s++) {
             double rel[3] = {sc[s][0] - env->cpos[0], sc[s][1] - env->cpos[1], sc[s][2] - env->cpos[2]}, loc[3];
             m3_tvec(Rc, rel, loc);
             double cl[3], dif[3], nl[3], dist;
@@ -573,6 +599,7 @@ static int gen_contacts(const po_config *cfg, const po_env *env, const okin *k, 
             }
             if (dist < PM_CONTACT_MARGIN_SPHERE) {
                 ocontact *c = &out[nc++];
+                nr++;
                 c->bodyA = SPH[s].link;
                 c->bodyB = -2;
                 m3_vec(Rc, nl, c->n);
@@ -587,36 +614,14 @@ static int gen_contacts(const po_config *cfg, const po_env *env, const okin *k, 
             }
         }
     }
-    if (cfg->has_cube) {
-        double h = cfg->cube_half;
-        int ng = 0;
-        for (int v = 0; v < 8 && ng < 4; v++) {
-            double loc[3] = {(v & 1) ? h : -h, (v & 2) ? h : -h, (v & 4) ? h : -h}, pw[3];
-            m3_vec(Rc, loc, pw);
-            for (int d = 0; d < 3; d++) pw[d] += env->cpos[d];
-            double top;
-            if (!ground_top(cfg, pw[0], pw[1], &top)) continue;
-            double dist = pw[2] - top;
-            if (dist < PM_CONTACT_MARGIN_GROUND) {
-                ocontact *c = &out[nc++];
-                ng++;
-                c->bodyA = -2;
-                c->bodyB = -1;
-                c->n[0] = 0; c->n[1] = 0; c->n[2] = 1;
-                memcpy(c->pA, pw, sizeof pw);
-                c->pB[0] = pw[0]; c->pB[1] = pw[1]; c->pB[2] = top;
-                c->dist = dist;
-                c->mu = PM_DEFAULT_FRICTION * PM_DEFAULT_FRICTION;
-            }
-        }
-    }
     if (cfg->has_robot) {
-        for (int s = 0; s < PM_NUM_SPHERES; s++) {
+        for (int s = 0; s < PM_NUM_SPHERES && nr < PM_MAX_ROBOT_CONTACTS; s++) {
             double top;
             if (!ground_top(cfg, sc[s][0], sc[s][1], &top)) continue;
             double dist = sc[s][2] - SPH[s].r - top;
             if (dist < PM_CONTACT_MARGIN_SPHERE) {
                 ocontact *c = &out[nc++];
+                nr++;
                 c->bodyA = SPH[s].link;
                 c->bodyB = -1;
                 c->n[0] = 0; c->n[1] = 0; c->n[2] = 1;
@@ -1100,13 +1105,14 @@ void po_reset(const po_config *cfg, po_env *env, int has_seed, uint64_t seed, fl
         double zr = cfg->task == PO_TASK_PICK_AND_PLACE ? 0.2 : 0.0;
         double n0 = uniform(env->rng, -0.15, 0.15), n1 = uniform(env->rng, -0.15, 0.15), n2 = uniform(env->rng, 0.0, zr);
         if (cfg->task == PO_TASK_PICK_AND_PLACE && po_pcg64_double(env->rng) < 0.3) n2 = 0.0;
+        /* object_size / 2 of the task (push.py:19), not the physics shape */
         env->goal[0] = 0.0 + n0;
         env->goal[1] = 0.0 + n1;
-        env->goal[2] = cfg->cube_half + n2;
+        env->goal[2] = PM_CUBE_HALF + n2;
         double o0 = uniform(env->rng, -0.15, 0.15), o1 = uniform(env->rng, -0.15, 0.15), o2 = uniform(env->rng, 0.0, 0.0);
         env->cpos[0] = 0.0 + o0;
         env->cpos[1] = 0.0 + o1;
-        env->cpos[2] = cfg->cube_half + o2;
+        env->cpos[2] = PM_CUBE_HALF + o2;
         env->cquat[0] = env->cquat[1] = env->cquat[2] = 0.0;
         env->cquat[3] = 1.0;
     }

@@ -1,0 +1,204 @@
+// ps_common.h — fp32 vector algebra and the compile-time Panda model for the
+// gfx950 kernels.  All model numbers come from include/panda_model.h; the URDF
+// origin rotations (multiples of pi/2 about x, -pi/4 about z) are made exact so
+// the compiler folds the 0/+-1 entries out of every frame product.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "panda_model.h"
+
+#define PS_D __device__ __forceinline__
+#define PS_HD __host__ __device__ __forceinline__
+
+namespace ps {
+
+// ------------------------------------------------------------------ vectors
+struct V3 {
+    float x, y, z;
+};
+PS_HD V3 mk(float x, float y, float z) { return V3{x, y, z}; }
+PS_HD V3 operator+(V3 a, V3 b) { return V3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+PS_HD V3 operator-(V3 a, V3 b) { return V3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+PS_HD V3 operator-(V3 a) { return V3{-a.x, -a.y, -a.z}; }
+PS_HD V3 operator*(V3 a, float s) { return V3{a.x * s, a.y * s, a.z * s}; }
+PS_HD V3 operator*(float s, V3 a) { return V3{a.x * s, a.y * s, a.z * s}; }
+PS_HD float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+PS_HD V3 cross(V3 a, V3 b) { return V3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+PS_D float norm(V3 a) { return sqrtf(dot(a, a)); }
+
+// row-major 3x3
+struct M3 {
+    float m[9];
+};
+PS_HD V3 col(const M3 &A, int c) { return V3{A.m[c], A.m[3 + c], A.m[6 + c]}; }
+PS_HD V3 mul(const M3 &A, V3 v) {
+    return V3{A.m[0] * v.x + A.m[1] * v.y + A.m[2] * v.z, A.m[3] * v.x + A.m[4] * v.y + A.m[5] * v.z,
+              A.m[6] * v.x + A.m[7] * v.y + A.m[8] * v.z};
+}
+PS_HD V3 tmul(const M3 &A, V3 v) {
+    return V3{A.m[0] * v.x + A.m[3] * v.y + A.m[6] * v.z, A.m[1] * v.x + A.m[4] * v.y + A.m[7] * v.z,
+              A.m[2] * v.x + A.m[5] * v.y + A.m[8] * v.z};
+}
+
+// symmetric 3x3 stored xx, yy, zz, xy, xz, yz
+struct S3 {
+    float xx, yy, zz, xy, xz, yz;
+};
+PS_HD V3 mul(const S3 &I, V3 v) {
+    return V3{I.xx * v.x + I.xy * v.y + I.xz * v.z, I.xy * v.x + I.yy * v.y + I.yz * v.z,
+              I.xz * v.x + I.yz * v.y + I.zz * v.z};
+}
+PS_HD S3 operator+(const S3 &a, const S3 &b) {
+    return S3{a.xx + b.xx, a.yy + b.yy, a.zz + b.zz, a.xy + b.xy, a.xz + b.xz, a.yz + b.yz};
+}
+// m * (|r|^2 E - r r^T)  (parallel-axis term)
+PS_HD S3 shift(float m, V3 r) {
+    return S3{m * (r.y * r.y + r.z * r.z), m * (r.x * r.x + r.z * r.z), m * (r.x * r.x + r.y * r.y),
+              -m * r.x * r.y, -m * r.x * r.z, -m * r.y * r.z};
+}
+// R diag(I) R^T
+PS_HD S3 rotate_diag(const M3 &R, float ix, float iy, float iz) {
+    const float *m = R.m;
+    return S3{m[0] * m[0] * ix + m[1] * m[1] * iy + m[2] * m[2] * iz,
+              m[3] * m[3] * ix + m[4] * m[4] * iy + m[5] * m[5] * iz,
+              m[6] * m[6] * ix + m[7] * m[7] * iy + m[8] * m[8] * iz,
+              m[0] * m[3] * ix + m[1] * m[4] * iy + m[2] * m[5] * iz,
+              m[0] * m[6] * ix + m[1] * m[7] * iy + m[2] * m[8] * iz,
+              m[3] * m[6] * ix + m[4] * m[7] * iy + m[5] * m[8] * iz};
+}
+
+// quaternion (x, y, z, w)
+struct Q4 {
+    float x, y, z, w;
+};
+PS_HD Q4 qmul(Q4 a, Q4 b) {
+    return Q4{a.w * b.x + a.x * b.w + a.y * b.z - a.z * b.y, a.w * b.y + a.y * b.w + a.z * b.x - a.x * b.z,
+              a.w * b.z + a.z * b.w + a.x * b.y - a.y * b.x, a.w * b.w - a.x * b.x - a.y * b.y - a.z * b.z};
+}
+PS_HD M3 quat_to_mat(Q4 q) {
+    float d = q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w, s = 2.0f / d;
+    float xs = q.x * s, ys = q.y * s, zs = q.z * s;
+    float wx = q.w * xs, wy = q.w * ys, wz = q.w * zs, xx = q.x * xs, xy = q.x * ys, xz = q.x * zs, yy = q.y * ys,
+          yz = q.y * zs, zz = q.z * zs;
+    return M3{{1.0f - (yy + zz), xy - wz, xz + wy, xy + wz, 1.0f - (xx + zz), yz - wx, xz - wy, yz + wx,
+               1.0f - (xx + yy)}};
+}
+// btMatrix3x3::getRotation
+PS_D Q4 mat_to_quat(const M3 &M) {
+    const float *m = M.m;
+    float tr = m[0] + m[4] + m[8];
+    Q4 q;
+    if (tr > 0.0f) {
+        float s = sqrtf(tr + 1.0f);
+        q.w = s * 0.5f;
+        s = 0.5f / s;
+        q.x = (m[7] - m[5]) * s;
+        q.y = (m[2] - m[6]) * s;
+        q.z = (m[3] - m[1]) * s;
+    } else if (m[0] < m[4] ? (m[4] < m[8]) : (m[0] < m[8])) {  // i = 2
+        float s = sqrtf(m[8] - m[0] - m[4] + 1.0f);
+        q.z = s * 0.5f;
+        s = 0.5f / s;
+        q.w = (m[3] - m[1]) * s;
+        q.x = (m[6] + m[2]) * s;
+        q.y = (m[7] + m[5]) * s;
+    } else if (m[0] < m[4]) {  // i = 1
+        float s = sqrtf(m[4] - m[8] - m[0] + 1.0f);
+        q.y = s * 0.5f;
+        s = 0.5f / s;
+        q.w = (m[2] - m[6]) * s;
+        q.z = (m[5] + m[7]) * s;
+        q.x = (m[3] + m[1]) * s;
+    } else {  // i = 0
+        float s = sqrtf(m[0] - m[4] - m[8] + 1.0f);
+        q.x = s * 0.5f;
+        s = 0.5f / s;
+        q.w = (m[7] - m[5]) * s;
+        q.y = (m[1] + m[3]) * s;
+        q.z = (m[2] + m[6]) * s;
+    }
+    return q;
+}
+
+// symmetric 9x9 packed lower-triangular index
+PS_HD constexpr int sidx(int i, int j) { return i >= j ? i * (i + 1) / 2 + j : j * (j + 1) / 2 + i; }
+
+// ---------------------------------------------------------------- the model
+struct LinkDef {
+    int parent, type, dof;
+    double o[3], rpy[3], axis[3];
+    double mass, com[3], aabb[3];
+};
+
+#define PS_LINKDEF(idx, par, typ, ox, oy, oz, rr, pp, yy, ax, ay, az, dof_, m, cx, cy, cz, bx, by, bz) \
+    LinkDef{par, typ, dof_, {ox, oy, oz}, {rr, pp, yy}, {ax, ay, az}, m, {cx, cy, cz}, {bx, by, bz}},
+
+PS_HD constexpr LinkDef link_def(int i) {
+    const LinkDef t[PM_NUM_LINKS] = {PM_LINK_TABLE(PS_LINKDEF)};
+    return t[i];
+}
+
+struct M3d {
+    double m[9];
+};
+// exact URDF origin rotations
+PS_HD constexpr M3d origin_rot(int i) {
+    LinkDef d = link_def(i);
+    if (d.rpy[0] == PM_HALF_PI_URDF) return M3d{{1, 0, 0, 0, 0, -1, 0, 1, 0}};
+    if (d.rpy[0] == -PM_HALF_PI_URDF) return M3d{{1, 0, 0, 0, 0, 1, 0, -1, 0}};
+    if (d.rpy[2] == -PM_QUARTER_PI_URDF) {
+        const double c = 0.70710678118654752440;
+        return M3d{{c, c, 0, -c, c, 0, 0, 0, 1}};
+    }
+    return M3d{{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+}
+PS_HD constexpr double link_inertia(int i, int axis) {
+    LinkDef d = link_def(i);
+    double lx = d.aabb[0], ly = d.aabb[1], lz = d.aabb[2];
+    return axis == 0 ? d.mass / 12.0 * (ly * ly + lz * lz)
+                     : (axis == 1 ? d.mass / 12.0 * (lx * lx + lz * lz) : d.mass / 12.0 * (lx * lx + ly * ly));
+}
+
+struct DofDef {
+    int link;
+    double lo, hi;
+};
+#define PS_DOFDEF(d, link, lo, hi) DofDef{link, lo, hi},
+PS_HD constexpr DofDef dof_def(int d) {
+    const DofDef t[PM_NUM_DOFS] = {PM_DOF_TABLE(PS_DOFDEF)};
+    return t[d];
+}
+
+struct SphereDef {
+    int link;
+    double c[3], r, mu;
+};
+#define PS_SPHDEF(link, x, y, z, r, mu) SphereDef{link, {x, y, z}, r, mu},
+PS_HD constexpr SphereDef sphere_def(int s) {
+    const SphereDef t[PM_NUM_SPHERES] = {PM_SPHERE_TABLE(PS_SPHDEF)};
+    return t[s];
+}
+
+PS_HD constexpr double joint_force(int d) {
+    const double f[PM_NUM_DOFS] = PM_JOINT_FORCES;
+    return f[d];
+}
+PS_HD constexpr double neutral_q(int d) {
+    const double f[PM_NUM_DOFS] = PM_NEUTRAL_Q;
+    return f[d];
+}
+
+// compile-time loop
+template <int B, int E, typename F>
+PS_D void static_for(F &&f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+}  // namespace ps

@@ -1,0 +1,844 @@
+// ps_physics.h — per-env (one env per lane) fp32 Panda multibody step for
+// gfx950.  Same algorithm as the PyBullet 3.2.5 subset used by
+// panda_gym/pybullet.py (restated in DESIGN.md §Physics), derived for a
+// register-resident lane:
+//   * forward kinematics with exact URDF origin rotations (12 links)
+//   * mass matrix by composite rigid bodies in the base frame, bias forces by
+//     a recursive Newton-Euler pass with prefix sums (gravity, gyroscopic,
+//     btMultiBody damping)
+//   * 9x9 Cholesky -> M^-1; joint-space rows (motors, limits) use columns of
+//     M^-1 directly; cube-ground rows act only on the cube's 6 DoF;
+//     gripper-contact rows carry explicit 9-wide Jacobians
+//   * projected Gauss-Seidel in btMultiBodyConstraintSolver order
+//   * semi-implicit Euler, exponential-map quaternion update.
+#pragma once
+
+#include "ps_common.h"
+
+namespace ps {
+
+struct Frame {
+    M3 R;
+    V3 o;
+};
+
+struct Kin {
+    Frame f[PM_NUM_LINKS];
+};
+
+// frame of link I given its parent frame and its joint coordinate
+template <int I>
+PS_D Frame child_frame(const Frame &P, float q) {
+    constexpr LinkDef d = link_def(I);
+    constexpr M3d Ro = origin_rot(I);
+    Frame F;
+    M3 Rj;
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+        for (int c = 0; c < 3; c++)
+            Rj.m[r * 3 + c] = P.R.m[r * 3 + 0] * (float)Ro.m[0 * 3 + c] + P.R.m[r * 3 + 1] * (float)Ro.m[1 * 3 + c] +
+                              P.R.m[r * 3 + 2] * (float)Ro.m[2 * 3 + c];
+    V3 oj = P.o + mul(P.R, mk((float)d.o[0], (float)d.o[1], (float)d.o[2]));
+    if constexpr (d.type == PM_JOINT_REVOLUTE) {
+        float s, c;
+        sincosf(q, &s, &c);
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            float a = Rj.m[r * 3 + 0], b = Rj.m[r * 3 + 1];
+            F.R.m[r * 3 + 0] = a * c + b * s;
+            F.R.m[r * 3 + 1] = b * c - a * s;
+            F.R.m[r * 3 + 2] = Rj.m[r * 3 + 2];
+        }
+        F.o = oj;
+    } else if constexpr (d.type == PM_JOINT_PRISMATIC) {
+        F.R = Rj;
+        V3 ax = mul(Rj, mk((float)d.axis[0], (float)d.axis[1], (float)d.axis[2]));
+        F.o = oj + ax * q;
+    } else {
+        F.R = Rj;
+        F.o = oj;
+    }
+    return F;
+}
+
+// all link frames, base-relative (robot base at the origin, identity rotation)
+PS_D void fk(const float q[9], Kin &k) {
+    Frame base;
+    base.R = M3{{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+    base.o = mk(0, 0, 0);
+    k.f[0] = child_frame<0>(base, q[0]);
+    k.f[1] = child_frame<1>(k.f[0], q[1]);
+    k.f[2] = child_frame<2>(k.f[1], q[2]);
+    k.f[3] = child_frame<3>(k.f[2], q[3]);
+    k.f[4] = child_frame<4>(k.f[3], q[4]);
+    k.f[5] = child_frame<5>(k.f[4], q[5]);
+    k.f[6] = child_frame<6>(k.f[5], q[6]);
+    k.f[7] = child_frame<7>(k.f[6], 0.0f);
+    k.f[8] = child_frame<8>(k.f[7], 0.0f);
+    k.f[9] = child_frame<9>(k.f[8], q[7]);
+    k.f[10] = child_frame<10>(k.f[8], q[8]);
+    k.f[11] = child_frame<11>(k.f[8], 0.0f);
+}
+
+// world axis of DoF d (revolute: frame z; prismatic: frame * axis)
+template <int D>
+PS_D V3 dof_axis(const Kin &k) {
+    constexpr int L = dof_def(D).link;
+    constexpr LinkDef d = link_def(L);
+    if constexpr (d.type == PM_JOINT_REVOLUTE) return col(k.f[L].R, 2);
+    else return mul(k.f[L].R, mk((float)d.axis[0], (float)d.axis[1], (float)d.axis[2]));
+}
+
+template <int I>
+PS_D V3 com_pos(const Kin &k) {
+    constexpr LinkDef d = link_def(I);
+    return k.f[I].o + mul(k.f[I].R, mk((float)d.com[0], (float)d.com[1], (float)d.com[2]));
+}
+
+// ------------------------------------------------------------------ dynamics
+struct Comp {
+    float m;
+    V3 h;  // COM
+    S3 I;  // about COM, base frame
+};
+
+template <int I>
+PS_D Comp link_comp(const Kin &k) {
+    constexpr LinkDef d = link_def(I);
+    Comp c;
+    c.m = (float)d.mass;
+    c.h = com_pos<I>(k);
+    c.I = rotate_diag(k.f[I].R, (float)link_inertia(I, 0), (float)link_inertia(I, 1), (float)link_inertia(I, 2));
+    return c;
+}
+
+PS_D Comp combine(const Comp &a, const Comp &b) {
+    Comp c;
+    c.m = a.m + b.m;
+    float inv = 1.0f / c.m;
+    c.h = (a.h * a.m + b.h * b.m) * inv;
+    c.I = a.I + b.I + shift(a.m, a.h - c.h) + shift(b.m, b.h - c.h);
+    return c;
+}
+
+// Joint-space mass matrix (packed symmetric, 45 floats) by composite rigid
+// bodies: for revolute b with composite C_b, the unit-rate momentum is
+// P = m_b a_b x (h_b - o_b), L = I_b a_b; M_ab = a_a . (L + (h_b - o_a) x P).
+PS_D void mass_matrix(const Kin &k, float M[45]) {
+    V3 ax[9], org[9];
+    static_for<0, 9>([&](auto D) {
+        constexpr int d = decltype(D)::value;
+        ax[d] = dof_axis<d>(k);
+        org[d] = k.f[dof_def(d).link].o;
+    });
+    Comp f9 = link_comp<9>(k), f10 = link_comp<10>(k);
+    // fingers (prismatic DoFs 7, 8)
+    {
+        V3 P9 = ax[7] * f9.m, P10 = ax[8] * f10.m;
+        M[sidx(7, 7)] = f9.m;
+        M[sidx(8, 8)] = f10.m;
+        M[sidx(8, 7)] = 0.0f;
+#pragma unroll
+        for (int a = 0; a < 7; a++) {
+            M[sidx(7, a)] = dot(ax[a], cross(f9.h - org[a], P9));
+            M[sidx(8, a)] = dot(ax[a], cross(f10.h - org[a], P10));
+        }
+    }
+    Comp c = combine(combine(link_comp<8>(k), f9), f10);
+    static_for<0, 7>([&](auto BB) {
+        constexpr int b = 6 - decltype(BB)::value;
+        c = combine(link_comp<b>(k), c);
+        V3 P = cross(ax[b], c.h - org[b]) * c.m;
+        V3 L = mul(c.I, ax[b]);
+#pragma unroll
+        for (int a = 0; a <= b; a++) M[sidx(b, a)] = dot(ax[a], L + cross(c.h - org[a], P));
+    });
+}
+
+// Bias forces h = C(q,qd) qd + g(q) + damping (RNEA with qdd = 0).  Forward
+// pass over the chain; every link force/moment is folded into prefix sums so
+// tau_i = a_i . ((N_tot - N_pre_i) - o_i x (F_tot - F_pre_i)) with moments
+// about the base origin.
+template <int I>
+PS_D void link_wrench(const Kin &k, V3 w, V3 dw, V3 vo, V3 ao, V3 &F, V3 &N) {
+    constexpr LinkDef d = link_def(I);
+    constexpr float m = (float)d.mass;
+    V3 c = com_pos<I>(k);
+    V3 rc = c - k.f[I].o;
+    V3 vc = vo + cross(w, rc);
+    V3 ac = ao + cross(dw, rc) + cross(w, cross(w, rc));
+    S3 Iw = rotate_diag(k.f[I].R, (float)link_inertia(I, 0), (float)link_inertia(I, 1), (float)link_inertia(I, 2));
+    V3 Iww = mul(Iw, w);
+    float cl = (float)PM_LINEAR_DAMPING + (float)PM_LINEAR_DAMPING * norm(vc);
+    float ca = (float)PM_ANGULAR_DAMPING + (float)PM_ANGULAR_DAMPING * norm(w);
+    F = (ac + vc * cl) * m;
+    V3 Nc = mul(Iw, dw) + cross(w, Iww) + Iww * ca;
+    N = Nc + cross(c, F);  // about the base origin
+}
+
+PS_D void bias_forces(const Kin &k, const float qd[9], float h[9]) {
+    V3 w = mk(0, 0, 0), dw = mk(0, 0, 0), vo = mk(0, 0, 0), ao = mk(0, 0, -(float)PM_GRAVITY_Z);
+    V3 prev_o = mk(0, 0, 0);
+    V3 Fpre[7], Npre[7];
+    V3 Fs = mk(0, 0, 0), Ns = mk(0, 0, 0);
+    V3 ax[7];
+    static_for<0, 7>([&](auto II) {
+        constexpr int I = decltype(II)::value;
+        V3 r = k.f[I].o - prev_o;
+        vo = vo + cross(w, r);
+        ao = ao + cross(dw, r) + cross(w, cross(w, r));
+        V3 a = col(k.f[I].R, 2);
+        ax[I] = a;
+        dw = dw + cross(w, a) * qd[I];
+        w = w + a * qd[I];
+        Fpre[I] = Fs;
+        Npre[I] = Ns;
+        V3 F, N;
+        link_wrench<I>(k, w, dw, vo, ao, F, N);
+        Fs = Fs + F;
+        Ns = Ns + N;
+        prev_o = k.f[I].o;
+    });
+    // link 7 (massless, fixed) and hand (8): same frame origin as link 7
+    {
+        V3 r = k.f[8].o - prev_o;
+        vo = vo + cross(w, r);
+        ao = ao + cross(dw, r) + cross(w, cross(w, r));
+        V3 F, N;
+        link_wrench<8>(k, w, dw, vo, ao, F, N);
+        Fs = Fs + F;
+        Ns = Ns + N;
+    }
+    // fingers: prismatic children of the hand
+    static_for<0, 2>([&](auto JJ) {
+        constexpr int J = decltype(JJ)::value;
+        constexpr int L = 9 + J;
+        V3 a = dof_axis<7 + J>(k);
+        float v = qd[7 + J];
+        V3 r = k.f[L].o - k.f[8].o;
+        V3 vf = vo + cross(w, r) + a * v;
+        V3 af = ao + cross(dw, r) + cross(w, cross(w, r)) + cross(w, a) * (2.0f * v);
+        V3 F, N;
+        link_wrench<L>(k, w, dw, vf, af, F, N);
+        h[7 + J] = dot(a, F);
+        Fs = Fs + F;
+        Ns = Ns + N;
+    });
+    static_for<0, 7>([&](auto II) {
+        constexpr int I = decltype(II)::value;
+        V3 Fsub = Fs - Fpre[I], Nsub = Ns - Npre[I];
+        h[I] = dot(ax[I], Nsub - cross(k.f[I].o, Fsub));
+    });
+}
+
+// M = L L^T, then M^-1 (packed symmetric) = L^-T L^-1
+PS_D void spd_inverse(float M[45]) {
+    float L[45];
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+#pragma unroll
+        for (int j = 0; j <= i; j++) {
+            float s = M[sidx(i, j)];
+#pragma unroll
+            for (int q = 0; q < j; q++) s -= L[sidx(i, q)] * L[sidx(j, q)];
+            if (i == j) L[sidx(i, i)] = sqrtf(s);
+            else L[sidx(i, j)] = s / L[sidx(j, j)];
+        }
+    }
+    // invert L in place (lower triangular)
+    float Li[45];
+#pragma unroll
+    for (int i = 0; i < 9; i++) {
+        float inv = 1.0f / L[sidx(i, i)];
+        Li[sidx(i, i)] = inv;
+#pragma unroll
+        for (int j = 0; j < i; j++) {
+            float s = 0.0f;
+#pragma unroll
+            for (int q = j; q < i; q++) s += L[sidx(i, q)] * Li[sidx(q, j)];
+            Li[sidx(i, j)] = -s * inv;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 9; i++)
+#pragma unroll
+        for (int j = 0; j <= i; j++) {
+            float s = 0.0f;
+#pragma unroll
+            for (int q = i; q < 9; q++) s += Li[sidx(q, i)] * Li[sidx(q, j)];
+            M[sidx(i, j)] = s;
+        }
+}
+
+// --------------------------------------------------------------------- IK
+// calculateInverseKinematics (restated in DESIGN.md §IK): <= 20 DLS steps
+// dq = (J^T J + 0.5 I)^-1 J^T [dp; dr], pivot-frame Jacobian, 45 deg clamp.
+template <int LINK>
+PS_D void inverse_kinematics(const float q_start[9], V3 target, Q4 orn, float q_out[9]) {
+    constexpr int NA = LINK <= 6 ? LINK + 1 : 7;  // arm DoFs that move LINK
+    constexpr bool FINGER = (LINK == 9 || LINK == 10);
+    constexpr int N = NA + (FINGER ? 1 : 0);
+    constexpr int FD = LINK == 9 ? 7 : 8;
+    float on = sqrtf(orn.x * orn.x + orn.y * orn.y + orn.z * orn.z + orn.w * orn.w);
+    Q4 ot = Q4{orn.x / on, orn.y / on, orn.z / on, orn.w / on};
+    float q[9];
+#pragma unroll
+    for (int d = 0; d < 9; d++) q[d] = q_start[d];
+    float diff = 1e30f;
+    for (int it = 0; it < PM_IK_MAX_ITERS && diff > (float)PM_IK_RESIDUAL; it++) {
+        Kin k;
+        fk(q, k);
+        V3 p = k.f[LINK].o;
+        V3 dS = target - p;
+        diff = norm(dS);
+        Q4 qe = mat_to_quat(k.f[LINK].R);
+        float n2 = qe.x * qe.x + qe.y * qe.y + qe.z * qe.z + qe.w * qe.w;
+        Q4 qinv = Q4{-qe.x / n2, -qe.y / n2, -qe.z / n2, qe.w / n2};
+        Q4 dq = qmul(ot, qinv);
+        // btQuaternion::getAngle()/getAxis() evaluate 2 acos(w) and
+        // v / sqrt(1 - w^2); for a unit quaternion these equal 2 atan2(|v|, w)
+        // and v / |v|, which stay accurate in fp32 when w -> 1 (acos would
+        // quantise small orientation errors to ~7e-4 rad).
+        float s2 = dq.x * dq.x + dq.y * dq.y + dq.z * dq.z;
+        float vn = sqrtf(s2);
+        float angle = 2.0f * atan2f(vn, dq.w);
+        V3 axv = s2 < 10.0f * 2.2204460492503131e-16f ? mk(1, 0, 0) : mk(dq.x, dq.y, dq.z) * (1.0f / vn);
+        if (angle > 3.14159265358979323846f) angle -= 6.28318530717958647692f;
+        else if (angle < -3.14159265358979323846f) angle += 6.28318530717958647692f;
+        V3 dR = axv * (angle / norm(axv));
+        // Jacobian columns (6 x N)
+        V3 Jv[N], Jw[N];
+#pragma unroll
+        for (int c = 0; c < NA; c++) {
+            V3 a = col(k.f[c].R, 2);
+            Jv[c] = cross(a, p - k.f[c].o);
+            Jw[c] = a;
+        }
+        if constexpr (FINGER) {
+            Jv[NA] = mul(k.f[LINK].R, mk(0.0f, LINK == 9 ? 1.0f : -1.0f, 0.0f));
+            Jw[NA] = mk(0, 0, 0);
+        }
+        float U[N * (N + 1) / 2], g[N];
+#pragma unroll
+        for (int a = 0; a < N; a++) {
+            g[a] = dot(Jv[a], dS) + dot(Jw[a], dR);
+#pragma unroll
+            for (int b = 0; b <= a; b++)
+                U[a * (a + 1) / 2 + b] = dot(Jv[a], Jv[b]) + dot(Jw[a], Jw[b]) + (a == b ? (float)PM_IK_DAMPING : 0.0f);
+        }
+        // Cholesky solve
+        float Lc[N * (N + 1) / 2];
+#pragma unroll
+        for (int i = 0; i < N; i++)
+#pragma unroll
+            for (int j = 0; j <= i; j++) {
+                float s = U[i * (i + 1) / 2 + j];
+#pragma unroll
+                for (int t = 0; t < j; t++) s -= Lc[i * (i + 1) / 2 + t] * Lc[j * (j + 1) / 2 + t];
+                if (i == j) Lc[i * (i + 1) / 2 + i] = sqrtf(s);
+                else Lc[i * (i + 1) / 2 + j] = s / Lc[j * (j + 1) / 2 + j];
+            }
+        float y[N], x[N];
+#pragma unroll
+        for (int i = 0; i < N; i++) {
+            float s = g[i];
+#pragma unroll
+            for (int t = 0; t < i; t++) s -= Lc[i * (i + 1) / 2 + t] * y[t];
+            y[i] = s / Lc[i * (i + 1) / 2 + i];
+        }
+#pragma unroll
+        for (int i = N - 1; i >= 0; i--) {
+            float s = y[i];
+#pragma unroll
+            for (int t = i + 1; t < N; t++) s -= Lc[t * (t + 1) / 2 + i] * x[t];
+            x[i] = s / Lc[i * (i + 1) / 2 + i];
+        }
+        float mx = 0.0f;
+#pragma unroll
+        for (int i = 0; i < N; i++) mx = fmaxf(mx, fabsf(x[i]));
+        float sc = mx > (float)PM_IK_MAX_ANGLE ? (float)PM_IK_MAX_ANGLE / mx : 1.0f;
+#pragma unroll
+        for (int i = 0; i < NA; i++) q[i] += x[i] * sc;
+        if constexpr (FINGER) q[FD] += x[NA] * sc;
+    }
+#pragma unroll
+    for (int d = 0; d < 9; d++) q_out[d] = q[d];
+}
+
+// ------------------------------------------------------------- the scene
+struct Scene {
+    V3 base;
+    float half, mass;
+    int has_table, has_plane, has_cube;
+};
+
+struct Motors {
+    float target[9], kp[9], kd[9], vel[9], imp[9];
+};
+
+struct Cube {
+    V3 pos;
+    Q4 quat;
+    V3 vel, omg;
+};
+
+PS_D bool ground_top(const Scene &sc, float x, float y, float &top) {
+    if (sc.has_table && fabsf(x - (float)PM_TABLE_CX) <= (float)PM_TABLE_HX && fabsf(y) <= (float)PM_TABLE_HY) {
+        top = (float)PM_TABLE_TOP;
+        return true;
+    }
+    if (sc.has_plane) {
+        top = (float)PM_PLANE_TOP;
+        return true;
+    }
+    return false;
+}
+
+// btPlaneSpace1
+PS_D void plane_space(V3 n, V3 &p, V3 &q) {
+    if (fabsf(n.z) > 0.70710678118654752f) {
+        float a = n.y * n.y + n.z * n.z, k = rsqrtf(a);
+        p = mk(0.0f, -n.z * k, n.y * k);
+        q = mk(a * k, -n.x * p.z, n.x * p.y);
+    } else {
+        float a = n.x * n.x + n.y * n.y, k = rsqrtf(a);
+        p = mk(-n.y * k, n.x * k, 0.0f);
+        q = mk(-n.z * p.y, n.z * p.x, a * k);
+    }
+}
+
+constexpr int NG = PM_MAX_GROUND_CONTACTS;
+constexpr int NR = PM_MAX_ROBOT_CONTACTS;
+
+// cube-ground contact: cube-only rows; normal +z, friction dirs of planeSpace(+z) = (0,-1,0), (1,0,0)
+struct GroundContact {
+    V3 r;  // contact point - cube COM
+    float rhs[3], lam[3], dinv[3];
+};
+
+// gripper contact: robot rows with explicit Jacobians; optional cube side
+struct RobotContact {
+    float J[3][9], MJ[3][9];
+    V3 dir[3];
+    V3 rB;  // cube side: point on cube - cube COM (valid if on_cube)
+    float rhs[3], lam[3], dinv[3], mu;
+    bool on_cube;
+};
+
+struct Solver {
+    float dv[9];
+    V3 dw, dvl;  // cube angular / linear velocity deltas
+};
+
+PS_D float jrow_dot(const float J[9], const float v[9]) {
+    float s = 0.0f;
+#pragma unroll
+    for (int d = 0; d < 9; d++) s += J[d] * v[d];
+    return s;
+}
+
+// ----------------------------------------------------------------- substep
+// One btMultiBodyDynamicsWorld::stepSimulation(1/500 s): see the oracle's
+// po_substep for the row-by-row restatement this mirrors.
+template <bool HAS_CUBE>
+PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cube &cb) {
+    const float dt = (float)PM_TIMESTEP;
+    Kin k;
+    fk(q, k);
+    float Mi[45], hb[9];
+    mass_matrix(k, Mi);
+    bias_forces(k, qd, hb);
+    spd_inverse(Mi);
+    float v1[9];
+#pragma unroll
+    for (int a = 0; a < 9; a++) {
+        float s = 0.0f;
+#pragma unroll
+        for (int b = 0; b < 9; b++) s -= Mi[sidx(a, b)] * hb[b];
+        v1[a] = qd[a] + dt * s;
+    }
+    // cube: gravity + btMultiBody damping (isotropic inertia: no gyroscopic term)
+    V3 cw1 = mk(0, 0, 0), cv1 = mk(0, 0, 0);
+    float inv_I = 0.0f, inv_m = 0.0f;
+    if constexpr (HAS_CUBE) {
+        float l = 2.0f * sc.half;
+        inv_I = 1.0f / (sc.mass / 12.0f * (2.0f * l * l));
+        inv_m = 1.0f / sc.mass;
+        float cl = (float)PM_LINEAR_DAMPING + (float)PM_LINEAR_DAMPING * norm(cb.vel);
+        float ca = (float)PM_ANGULAR_DAMPING + (float)PM_ANGULAR_DAMPING * norm(cb.omg);
+        cv1 = cb.vel + (mk(0, 0, (float)PM_GRAVITY_Z) - cb.vel * cl) * dt;
+        cw1 = cb.omg - cb.omg * (ca * dt);
+    }
+
+    // ---- joint-space rows: limits (lower/upper) and motors
+    float dinvj[9];
+    float lim_rhs[9][2], lim_lam[9][2];
+    bool lim_on[9][2];
+    float split_dq[9];
+    float mot_rhs[9], mot_lam[9];
+#pragma unroll
+    for (int d = 0; d < 9; d++) {
+        float den = Mi[sidx(d, d)];
+        dinvj[d] = den > 2.2204460492503131e-16f ? 1.0f / den : 0.0f;
+        split_dq[d] = 0.0f;
+#pragma unroll
+        for (int side = 0; side < 2; side++) {
+            float lo = (float)dof_def(d).lo, hi = (float)dof_def(d).hi;
+            float pen = side ? hi - q[d] : q[d] - lo;
+            float sgn = side ? -1.0f : 1.0f;
+            lim_on[d][side] = pen <= 0.0f;
+            float velerr = -sgn * v1[d];
+            bool combined = pen > (float)PM_SPLIT_PENETRATION_THRESHOLD;
+            float poserr = -pen * (float)PM_ERP / dt;
+            lim_rhs[d][side] = (combined ? poserr + velerr : velerr) * dinvj[d];
+            lim_lam[d][side] = 0.0f;
+            if (lim_on[d][side] && !combined) split_dq[d] += sgn * (-pen) * (float)PM_SPLIT_LIMIT_ERP;
+        }
+        float target = mt.kp[d] * (mt.target[d] - q[d]) / dt + v1[d] + mt.kd[d] * (mt.vel[d] - v1[d]);
+        mot_rhs[d] = (target - v1[d]) * dinvj[d];
+        mot_lam[d] = 0.0f;
+    }
+
+    // ---- contacts
+    GroundContact gc[NG];
+    int ng = 0;
+    RobotContact rc[NR];
+    int nr = 0;
+    M3 Rc;
+    if constexpr (HAS_CUBE) {
+        Rc = quat_to_mat(cb.quat);
+        const float h = sc.half;
+#pragma unroll
+        for (int v = 0; v < 8; v++) {
+            V3 loc = mk((v & 1) ? h : -h, (v & 2) ? h : -h, (v & 4) ? h : -h);
+            V3 pw = cb.pos + mul(Rc, loc);
+            float top;
+            if (ng < NG && ground_top(sc, pw.x, pw.y, top)) {
+                float dist = pw.z - top;
+                if (dist < (float)PM_CONTACT_MARGIN_GROUND) {
+                    V3 r = pw - cb.pos;
+                    // normal (0,0,1), t1 (0,-1,0), t2 (1,0,0)
+                    V3 dirs[3] = {mk(0, 0, 1), mk(0, -1, 0), mk(1, 0, 0)};
+                    GroundContact g;
+                    g.r = r;
+#pragma unroll
+                    for (int j = 0; j < 3; j++) {
+                        V3 rn = cross(r, dirs[j]);
+                        float den = dot(rn, rn) * inv_I + dot(dirs[j], dirs[j]) * inv_m;
+                        g.dinv[j] = den > 2.2204460492503131e-16f ? 1.0f / den : 0.0f;
+                        float rel = dot(rn, cw1) + dot(dirs[j], cv1);
+                        g.lam[j] = 0.0f;
+                        if (j == 0) {
+                            float pen = dist + (float)PM_LINEAR_SLOP;
+                            float velerr = -rel, poserr = 0.0f;
+                            if (pen > 0.0f) velerr -= pen / dt;
+                            else poserr = -pen * (float)PM_ERP / dt;
+                            bool combined = pen > (float)PM_SPLIT_PENETRATION_THRESHOLD;
+                            g.rhs[0] = (combined ? poserr + velerr : velerr) * g.dinv[0];
+                        } else {
+                            g.rhs[j] = -rel * g.dinv[j];
+                        }
+                    }
+#pragma unroll
+                    for (int s = 0; s < NG; s++)
+                        if (s == ng) gc[s] = g;
+                    ng++;
+                }
+            }
+        }
+    }
+    {
+        // gripper spheres (base-relative frames -> world)
+        V3 spw[PM_NUM_SPHERES];
+        static_for<0, PM_NUM_SPHERES>([&](auto SS) {
+            constexpr int S = decltype(SS)::value;
+            constexpr SphereDef s = sphere_def(S);
+            spw[S] = k.f[s.link].o + mul(k.f[s.link].R, mk((float)s.c[0], (float)s.c[1], (float)s.c[2])) + sc.base;
+        });
+        auto add_robot = [&](int link, V3 pA, V3 n, float dist, float mu, bool on_cube, V3 pB) {
+            RobotContact c;
+            plane_space(n, c.dir[1], c.dir[2]);
+            c.dir[0] = n;
+            c.on_cube = on_cube;
+            c.rB = pB - cb.pos;
+            c.mu = mu;
+            V3 p = pA - sc.base;
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                V3 dj = c.dir[j];
+                static_for<0, 7>([&](auto DD) {
+                    constexpr int D = decltype(DD)::value;
+                    V3 a = col(k.f[D].R, 2);
+                    c.J[j][D] = dot(a, cross(p - k.f[D].o, dj));
+                });
+                c.J[j][7] = link == 9 ? dot(dof_axis<7>(k), dj) : 0.0f;
+                c.J[j][8] = link == 10 ? dot(dof_axis<8>(k), dj) : 0.0f;
+#pragma unroll
+                for (int a = 0; a < 9; a++) {
+                    float s = 0.0f;
+#pragma unroll
+                    for (int b = 0; b < 9; b++) s += Mi[sidx(a, b)] * c.J[j][b];
+                    c.MJ[j][a] = s;
+                }
+                float den = jrow_dot(c.J[j], c.MJ[j]);
+                float rel = jrow_dot(c.J[j], v1);
+                if (on_cube) {
+                    V3 rn = cross(c.rB, dj);
+                    den += dot(rn, rn) * inv_I + dot(dj, dj) * inv_m;
+                    rel -= dot(rn, cw1) + dot(dj, cv1);
+                }
+                c.dinv[j] = den > 2.2204460492503131e-16f ? 1.0f / den : 0.0f;
+                c.lam[j] = 0.0f;
+                if (j == 0) {
+                    float pen = dist + (float)PM_LINEAR_SLOP;
+                    float velerr = -rel, poserr = 0.0f;
+                    if (pen > 0.0f) velerr -= pen / dt;
+                    else poserr = -pen * (float)PM_ERP / dt;
+                    bool combined = pen > (float)PM_SPLIT_PENETRATION_THRESHOLD;
+                    c.rhs[0] = (combined ? poserr + velerr : velerr) * c.dinv[0];
+                } else {
+                    c.rhs[j] = -rel * c.dinv[j];
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < NR; s++)
+                if (s == nr) rc[s] = c;
+            nr++;
+        };
+        if constexpr (HAS_CUBE) {
+            const float h = sc.half;
+            static_for<0, PM_NUM_SPHERES>([&](auto SS) {
+                constexpr int S = decltype(SS)::value;
+                constexpr SphereDef s = sphere_def(S);
+                if (nr < NR) {
+                    V3 loc = tmul(Rc, spw[S] - cb.pos);
+                    V3 cl = mk(fminf(fmaxf(loc.x, -h), h), fminf(fmaxf(loc.y, -h), h), fminf(fmaxf(loc.z, -h), h));
+                    V3 dif = loc - cl;
+                    float dn = norm(dif);
+                    V3 nl;
+                    float dist;
+                    if (dn > 1e-9f) {
+                        nl = dif * (1.0f / dn);
+                        dist = dn - (float)s.r;
+                    } else {
+                        float bx = h - fabsf(loc.x), by = h - fabsf(loc.y), bz = h - fabsf(loc.z);
+                        int ax = 0;
+                        float best = bx;
+                        if (by < best) { best = by; ax = 1; }
+                        if (bz < best) { best = bz; ax = 2; }
+                        float sg;
+                        if (ax == 0) { sg = loc.x >= 0.0f ? 1.0f : -1.0f; nl = mk(sg, 0, 0); cl.x = sg * h; }
+                        else if (ax == 1) { sg = loc.y >= 0.0f ? 1.0f : -1.0f; nl = mk(0, sg, 0); cl.y = sg * h; }
+                        else { sg = loc.z >= 0.0f ? 1.0f : -1.0f; nl = mk(0, 0, sg); cl.z = sg * h; }
+                        dist = -best - (float)s.r;
+                    }
+                    if (dist < (float)PM_CONTACT_MARGIN_SPHERE) {
+                        V3 n = mul(Rc, nl);
+                        V3 pB = cb.pos + mul(Rc, cl);
+                        V3 pA = spw[S] - n * (float)s.r;
+                        add_robot(s.link, pA, n, dist, (float)(s.mu * PM_DEFAULT_FRICTION), true, pB);
+                    }
+                }
+            });
+        }
+        static_for<0, PM_NUM_SPHERES>([&](auto SS) {
+            constexpr int S = decltype(SS)::value;
+            constexpr SphereDef s = sphere_def(S);
+            float top;
+            if (nr < NR && ground_top(sc, spw[S].x, spw[S].y, top)) {
+                float dist = spw[S].z - (float)s.r - top;
+                if (dist < (float)PM_CONTACT_MARGIN_SPHERE) {
+                    V3 pA = spw[S] - mk(0, 0, (float)s.r);
+                    add_robot(s.link, pA, mk(0, 0, 1), dist, (float)(s.mu * PM_DEFAULT_FRICTION), false, pA);
+                }
+            }
+        });
+    }
+
+    // ---- projected Gauss-Seidel
+    Solver S;
+#pragma unroll
+    for (int d = 0; d < 9; d++) S.dv[d] = 0.0f;
+    S.dw = mk(0, 0, 0);
+    S.dvl = mk(0, 0, 0);
+
+    auto joint_row = [&](int d, float sgn, float rhs, float &lam, float lo, float hi) -> float {
+        float dl = rhs - dinvj[d] * (sgn * S.dv[d]);
+        float sum = lam + dl;
+        if (sum < lo) { dl = lo - lam; lam = lo; }
+        else if (sum > hi) { dl = hi - lam; lam = hi; }
+        else lam = sum;
+        float f = sgn * dl;
+#pragma unroll
+        for (int a = 0; a < 9; a++) S.dv[a] += Mi[sidx(a, d)] * f;
+        return dinvj[d] != 0.0f ? dl / dinvj[d] : 0.0f;
+    };
+
+    for (int it = 0; it < PM_SOLVER_ITERATIONS; it++) {
+        float res = 0.0f, x;
+        if (it & 1) {
+#pragma unroll
+            for (int d = 0; d < 9; d++)
+#pragma unroll
+                for (int side = 0; side < 2; side++)
+                    if (lim_on[d][side]) {
+                        x = joint_row(d, side ? -1.0f : 1.0f, lim_rhs[d][side], lim_lam[d][side], 0.0f,
+                                      (float)PM_LIMIT_MAX_IMPULSE);
+                        res = fmaxf(res, x * x);
+                    }
+#pragma unroll
+            for (int d = 0; d < 9; d++)
+                if (mt.imp[d] != 0.0f) {
+                    x = joint_row(d, 1.0f, mot_rhs[d], mot_lam[d], -mt.imp[d], mt.imp[d]);
+                    res = fmaxf(res, x * x);
+                }
+        } else {
+#pragma unroll
+            for (int d = 8; d >= 0; d--)
+                if (mt.imp[d] != 0.0f) {
+                    x = joint_row(d, 1.0f, mot_rhs[d], mot_lam[d], -mt.imp[d], mt.imp[d]);
+                    res = fmaxf(res, x * x);
+                }
+#pragma unroll
+            for (int d = 8; d >= 0; d--)
+#pragma unroll
+                for (int side = 1; side >= 0; side--)
+                    if (lim_on[d][side]) {
+                        x = joint_row(d, side ? -1.0f : 1.0f, lim_rhs[d][side], lim_lam[d][side], 0.0f,
+                                      (float)PM_LIMIT_MAX_IMPULSE);
+                        res = fmaxf(res, x * x);
+                    }
+        }
+        // normals: ground contacts then gripper contacts
+        if constexpr (HAS_CUBE) {
+#pragma unroll
+            for (int c = 0; c < NG; c++)
+                if (c < ng) {
+                    GroundContact &g = gc[c];
+                    V3 rn = mk(g.r.y, -g.r.x, 0.0f);  // r x (0,0,1)
+                    float dl = g.rhs[0] - g.dinv[0] * (dot(rn, S.dw) + S.dvl.z);
+                    float sum = g.lam[0] + dl;
+                    if (sum < 0.0f) { dl = -g.lam[0]; g.lam[0] = 0.0f; }
+                    else if (sum > (float)PM_CONTACT_UPPER) { dl = (float)PM_CONTACT_UPPER - g.lam[0]; g.lam[0] = (float)PM_CONTACT_UPPER; }
+                    else g.lam[0] = sum;
+                    S.dw = S.dw + rn * (dl * inv_I);
+                    S.dvl.z += dl * inv_m;
+                    x = g.dinv[0] != 0.0f ? dl / g.dinv[0] : 0.0f;
+                    res = fmaxf(res, x * x);
+                }
+        }
+#pragma unroll
+        for (int c = 0; c < NR; c++)
+            if (c < nr) {
+                RobotContact &r = rc[c];
+                float jv = jrow_dot(r.J[0], S.dv);
+                V3 rn;
+                if (HAS_CUBE && r.on_cube) {
+                    rn = cross(r.rB, r.dir[0]);
+                    jv -= dot(rn, S.dw) + dot(r.dir[0], S.dvl);
+                }
+                float dl = r.rhs[0] - r.dinv[0] * jv;
+                float sum = r.lam[0] + dl;
+                if (sum < 0.0f) { dl = -r.lam[0]; r.lam[0] = 0.0f; }
+                else if (sum > (float)PM_CONTACT_UPPER) { dl = (float)PM_CONTACT_UPPER - r.lam[0]; r.lam[0] = (float)PM_CONTACT_UPPER; }
+                else r.lam[0] = sum;
+#pragma unroll
+                for (int a = 0; a < 9; a++) S.dv[a] += r.MJ[0][a] * dl;
+                if (HAS_CUBE && r.on_cube) {
+                    S.dw = S.dw - rn * (dl * inv_I);
+                    S.dvl = S.dvl - r.dir[0] * (dl * inv_m);
+                }
+                x = r.dinv[0] != 0.0f ? dl / r.dinv[0] : 0.0f;
+                res = fmaxf(res, x * x);
+            }
+        // friction cones
+        if constexpr (HAS_CUBE) {
+#pragma unroll
+            for (int c = 0; c < NG; c++)
+                if (c < ng) {
+                    GroundContact &g = gc[c];
+                    V3 r1 = mk(g.r.z, 0.0f, -g.r.x);  // r x (0,-1,0)
+                    V3 r2 = mk(0.0f, g.r.z, -g.r.y);  // r x (1,0,0)
+                    float dla = g.rhs[1] - g.dinv[1] * (dot(r1, S.dw) - S.dvl.y);
+                    float dlb = g.rhs[2] - g.dinv[2] * (dot(r2, S.dw) + S.dvl.x);
+                    float sa = g.lam[1] + dla, sb = g.lam[2] + dlb;
+                    float lim = (float)(PM_DEFAULT_FRICTION * PM_DEFAULT_FRICTION) * fmaxf(g.lam[0], 0.0f);
+                    float mag = sqrtf(sa * sa + sb * sb);
+                    if (mag > lim) {
+                        float s = mag > 0.0f ? lim / mag : 0.0f;
+                        sa *= s;
+                        sb *= s;
+                    }
+                    dla = sa - g.lam[1];
+                    dlb = sb - g.lam[2];
+                    g.lam[1] = sa;
+                    g.lam[2] = sb;
+                    S.dw = S.dw + (r1 * dla + r2 * dlb) * inv_I;
+                    S.dvl = S.dvl + mk(dlb, -dla, 0.0f) * inv_m;
+                    float ra = g.dinv[1] != 0.0f ? dla / g.dinv[1] : 0.0f;
+                    float rb = g.dinv[2] != 0.0f ? dlb / g.dinv[2] : 0.0f;
+                    x = fabsf(ra) > fabsf(rb) ? ra : rb;
+                    res = fmaxf(res, x * x);
+                }
+        }
+#pragma unroll
+        for (int c = 0; c < NR; c++)
+            if (c < nr) {
+                RobotContact &r = rc[c];
+                float ja = jrow_dot(r.J[1], S.dv), jb = jrow_dot(r.J[2], S.dv);
+                V3 r1, r2;
+                if (HAS_CUBE && r.on_cube) {
+                    r1 = cross(r.rB, r.dir[1]);
+                    r2 = cross(r.rB, r.dir[2]);
+                    ja -= dot(r1, S.dw) + dot(r.dir[1], S.dvl);
+                    jb -= dot(r2, S.dw) + dot(r.dir[2], S.dvl);
+                }
+                float dla = r.rhs[1] - r.dinv[1] * ja, dlb = r.rhs[2] - r.dinv[2] * jb;
+                float sa = r.lam[1] + dla, sb = r.lam[2] + dlb;
+                float lim = r.mu * fmaxf(r.lam[0], 0.0f);
+                float mag = sqrtf(sa * sa + sb * sb);
+                if (mag > lim) {
+                    float s = mag > 0.0f ? lim / mag : 0.0f;
+                    sa *= s;
+                    sb *= s;
+                }
+                dla = sa - r.lam[1];
+                dlb = sb - r.lam[2];
+                r.lam[1] = sa;
+                r.lam[2] = sb;
+#pragma unroll
+                for (int a = 0; a < 9; a++) S.dv[a] += r.MJ[1][a] * dla + r.MJ[2][a] * dlb;
+                if (HAS_CUBE && r.on_cube) {
+                    S.dw = S.dw - (r1 * dla + r2 * dlb) * inv_I;
+                    S.dvl = S.dvl - (r.dir[1] * dla + r.dir[2] * dlb) * inv_m;
+                }
+                float ra = r.dinv[1] != 0.0f ? dla / r.dinv[1] : 0.0f;
+                float rb = r.dinv[2] != 0.0f ? dlb / r.dinv[2] : 0.0f;
+                x = fabsf(ra) > fabsf(rb) ? ra : rb;
+                res = fmaxf(res, x * x);
+            }
+        if (res <= (float)PM_SOLVER_RESIDUAL_THRESHOLD) break;
+    }
+
+    // ---- integrate (btMultiBody::stepPositionsMultiDof)
+#pragma unroll
+    for (int d = 0; d < 9; d++) {
+        qd[d] = v1[d] + S.dv[d];
+        q[d] += dt * qd[d] + split_dq[d];
+    }
+    if constexpr (HAS_CUBE) {
+        cb.omg = cw1 + S.dw;
+        cb.vel = cv1 + S.dvl;
+        cb.pos = cb.pos + cb.vel * dt;
+        float ang = norm(cb.omg);
+        if (ang * dt > 0.5f * 1.5707963267948966f) ang = 0.5f * 1.5707963267948966f / dt;
+        float f = ang < 0.001f ? (0.5f * dt - (dt * dt * dt) * 0.020833333333f * ang * ang) : sinf(0.5f * ang * dt) / ang;
+        Q4 dq = Q4{cb.omg.x * f, cb.omg.y * f, cb.omg.z * f, cosf(0.5f * ang * dt)};
+        Q4 nq = qmul(dq, cb.quat);
+        float nn = rsqrtf(nq.x * nq.x + nq.y * nq.y + nq.z * nq.z + nq.w * nq.w);
+        cb.quat = Q4{nq.x * nn, nq.y * nn, nq.z * nn, nq.w * nn};
+    }
+}
+
+}  // namespace ps

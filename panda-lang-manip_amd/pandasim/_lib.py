@@ -1,0 +1,104 @@
+"""ctypes binding of libpandasim.so (include/pandasim.h).
+
+The library is built in-tree (``python -m pandasim.build`` or
+``__graft_entry__.build()``) and loaded from this package directory.  There is
+no CPU fallback: if the library or a GPU is missing, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpandasim.so")
+
+PS_OK = 0
+ERRORS = {-1: "PS_ERR_ARG", -2: "PS_ERR_HIP", -3: "PS_ERR_UNSUPPORTED"}
+
+# float row indices of the SoA state (include/pandasim.h)
+F_Q, F_QD, F_MTARGET, F_MKP, F_MKD, F_MVEL, F_MIMP = 0, 9, 18, 27, 36, 45, 54
+F_CPOS, F_CQUAT, F_CVEL, F_COMG = 63, 66, 70, 73
+NUM_FLOAT_ROWS = 76
+
+
+class Config(C.Structure):
+    _fields_ = [
+        ("task", C.c_int32), ("control", C.c_int32), ("reward", C.c_int32), ("block_gripper", C.c_int32),
+        ("has_table", C.c_int32), ("has_plane", C.c_int32), ("has_cube", C.c_int32), ("reserved", C.c_int32),
+        ("base", C.c_float * 3), ("cube_half", C.c_float), ("cube_mass", C.c_float),
+    ]
+
+
+class Layout(C.Structure):
+    _fields_ = [
+        ("num_envs", C.c_int64), ("stride", C.c_int64), ("float_offset", C.c_int64), ("goal_offset", C.c_int64),
+        ("rng_offset", C.c_int64), ("elapsed_offset", C.c_int64), ("total_bytes", C.c_int64),
+    ]
+
+
+class PandasimError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def exported_symbols():
+    return [
+        "ps_abi_version", "ps_default_config", "ps_state_layout", "ps_create", "ps_destroy", "ps_last_error",
+        "ps_obs_dim", "ps_action_dim", "ps_init_state", "ps_reset", "ps_step", "ps_sim_step", "ps_link_state",
+        "ps_inverse_kinematics", "ps_compute_reward",
+    ]
+
+
+def lib():
+    """Load libpandasim.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PandasimError(f"{LIB_PATH} not found: build it with `python -m pandasim.build` (hipcc, gfx950)")
+    L = C.CDLL(LIB_PATH)
+    V, I, I64, P = C.c_void_p, C.c_int, C.c_int64, C.POINTER
+    L.ps_abi_version.restype = I
+    L.ps_default_config.argtypes = [I, I, I, P(Config)]
+    L.ps_state_layout.argtypes = [I64, P(Layout)]
+    L.ps_create.argtypes = [P(Config), I64, I, P(V)]
+    L.ps_destroy.argtypes = [V]
+    L.ps_destroy.restype = None
+    L.ps_last_error.argtypes = [V]
+    L.ps_last_error.restype = C.c_char_p
+    L.ps_obs_dim.argtypes = [V]
+    L.ps_action_dim.argtypes = [V]
+    L.ps_init_state.argtypes = [V, V, V]
+    L.ps_reset.argtypes = [V, V, V, V, V, V, V, V]
+    L.ps_step.argtypes = [V, V, V, V, V, V, V, V, V, I, V, V, V]
+    L.ps_sim_step.argtypes = [V, V, I, V]
+    L.ps_link_state.argtypes = [V, V, I, V, V, V, V, V]
+    L.ps_inverse_kinematics.argtypes = [V, V, I, V, V, V, V]
+    L.ps_compute_reward.argtypes = [I, V, I, V, I, V, V, I64, V]
+    for name in exported_symbols():
+        getattr(L, name).restype = getattr(L, name).restype if name in ("ps_destroy", "ps_last_error") else I
+    _lib = L
+    return L
+
+
+def check(rc: int, ctx=None, what: str = "") -> None:
+    if rc != PS_OK:
+        msg = ""
+        if ctx is not None:
+            raw = lib().ps_last_error(ctx)
+            msg = raw.decode() if raw else ""
+        raise PandasimError(f"{what} failed: {ERRORS.get(rc, rc)} {msg}".strip())
+
+
+def layout(num_envs: int) -> Layout:
+    lay = Layout()
+    check(lib().ps_state_layout(int(num_envs), C.byref(lay)), what="ps_state_layout")
+    return lay
+
+
+def default_config(task: int, control: int, reward: int) -> Config:
+    cfg = Config()
+    check(lib().ps_default_config(task, control, reward, C.byref(cfg)), what="ps_default_config")
+    return cfg

@@ -1,0 +1,38 @@
+"""Build libpandasim.so in-tree with hipcc for gfx950 (no JIT, no torch extension)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+CSRC = os.path.join(os.path.dirname(HERE), "csrc")
+OUT = os.path.join(HERE, "libpandasim.so")
+SOURCES = ["pandasim.hip"]
+DEPS = ["pandasim.hip", "ps_common.h", "ps_physics.h", "ps_task.h"]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("pandasim.h", "panda_model.h")]
+
+
+def needs_build() -> bool:
+    if not os.path.exists(OUT):
+        return True
+    t = os.path.getmtime(OUT)
+    return any(os.path.getmtime(p) > t for p in [os.path.join(CSRC, d) for d in DEPS] + HEADERS)
+
+
+def build(force: bool = False, verbose: bool = True) -> str:
+    if not force and not needs_build():
+        return OUT
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I", os.path.join(ROOT, "include"),
+           "-o", OUT + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

@@ -1,0 +1,319 @@
+"""GPU parity tests: the HIP path (through libpandasim.so's C ABI) against the
+fp64 CPU oracle and the reference's golden vectors / known-answer tests.
+
+Tolerances (fp32 kernel vs fp64 oracle; BASELINE north star: 1e-3):
+  * task layer (goal/object sampling, rewards, success, TimeLimit): bit-exact;
+  * KATs: atol 1e-3 as in /root/reference/test/pybullet_test.py;
+  * engine step (20 substeps) from identical state + motors: joint positions
+    2e-4, joint velocities 5e-3, object position 5e-4;
+  * IK: median 1e-5 rad, max 2e-3 rad (the 1e-4 stopping rule);
+  * fused env step from identical state: positions 5e-4, velocities 2e-2
+    (velocity = 50/s x IK target error).
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import oracle_config_for, oracle_env_from, snapshot
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TASKS = [("reach", "ee"), ("reach", "joints"), ("push", "ee"), ("push", "joints"), ("pick_and_place", "ee"),
+         ("pick_and_place", "joints")]
+
+
+@pytest.fixture(scope="module")
+def ps():
+    import pandasim
+
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return pandasim
+
+
+def make_env(ps, task, control, n, reward="sparse"):
+    from pandasim.envs import PandaVecEnv
+
+    return PandaVecEnv(task, reward, control, n, "cuda")
+
+
+# ------------------------------------------------------------ known answers
+def kat_sim(ps, **overrides):
+    from pandasim import _lib as L
+    from pandasim.sim import PandaSim
+
+    cfg = L.default_config(0, 0, 0)
+    cfg.has_table = cfg.has_plane = 0
+    cfg.base[0] = 0.0
+    for k, v in overrides.items():
+        setattr(cfg, k, v)
+    return PandaSim(config=cfg, num_envs=4)
+
+
+def test_kat_link_position(ps):  # pybullet_test.py:124-136
+    sim = kat_sim(ps)
+    pos = sim.get_link_position("panda", 1).cpu().numpy()
+    assert np.allclose(pos, [0.0, 0.060, 0.373], atol=1e-3)
+
+
+def test_kat_joint5_motor(ps):  # pybullet_test.py:139-204
+    sim = kat_sim(ps)
+    sim.control_joints("panda", [5], [0.3], [5.0])
+    sim.step()
+    pos, orn, v, w = [t.cpu().numpy() for t in sim.link_state(5)]
+    assert np.allclose(orn, [0.707, -0.02, 0.02, 0.707], atol=1e-3)
+    assert np.allclose(v, [-0.0068, 0.0000, 0.1186], atol=1e-3)
+    assert np.allclose(w, [0.000, -2.969, 0.000], atol=1e-3)
+    assert np.allclose(sim.get_joint_angle("panda", 5).cpu().numpy(), 0.063, atol=1e-3)
+
+
+def test_kat_inverse_kinematics(ps):  # pybullet_test.py:254-266
+    sim = kat_sim(ps)
+    q = sim.inverse_kinematics("panda", 6, [0.4, 0.5, 0.6], [0.707, -0.02, 0.02, 0.707]).cpu().numpy()
+    assert np.allclose(q, [1.000, 1.223, -1.113, -0.021, -0.917, 0.666, -0.499, 0.0, 0.0], atol=1e-3)
+
+
+def test_kat_box_free_fall(ps):  # pybullet_test.py:56-64 (robot parked far away: no contact)
+    from pandasim import _lib as L
+    from pandasim.sim import PandaSim
+
+    cfg = L.default_config(1, 0, 0)
+    cfg.has_table = cfg.has_plane = 0
+    cfg.base[0] = 10.0
+    cfg.cube_half = 0.5
+    sim = PandaSim(config=cfg, num_envs=4)
+    sim.step()
+    assert np.allclose(sim.get_base_velocity("my_box").cpu().numpy(), [0.0, 0.0, -0.392], atol=1e-3)
+    assert np.allclose(sim.get_base_orientation("my_box").cpu().numpy(), [0, 0, 0, 1], atol=1e-3)
+
+
+# ------------------------------------------------------------ task layer
+@pytest.mark.parametrize("task", ["reach", "push", "pick_and_place"])
+def test_reset_goldens_bit_exact(ps, golden, task):
+    seeds = golden["seeds"]
+    env = make_env(ps, task, "ee", len(seeds))
+    for r in range(golden[f"{task}_goal"].shape[1]):
+        obs, _ = env.reset(seed=seeds if r == 0 else None)
+        goal = env.sim.goal[:, :len(seeds)].t().cpu().numpy()
+        assert np.array_equal(goal, golden[f"{task}_goal"][:, r])
+        assert np.array_equal(obs["desired_goal"].cpu().numpy(), golden[f"{task}_goal"][:, r].astype(np.float32))
+        if task != "reach":
+            cpos = env.sim.get_base_position("object").cpu().numpy()
+            assert np.array_equal(cpos, golden[f"{task}_object"][:, r].astype(np.float32))
+
+
+def test_compute_reward_goldens_bit_exact(ps, golden):
+    for reward_type in ["sparse", "dense"]:
+        env = make_env(ps, "push", "ee", 8, reward=reward_type)
+        ag = torch.from_numpy(golden["reward_ag"]).cuda()
+        dg = torch.from_numpy(golden["reward_dg"]).cuda()
+        r = env.compute_reward(ag, dg, {}).cpu().numpy()
+        assert np.array_equal(r.view(np.uint32), golden[f"reward_{reward_type}"].view(np.uint32))
+        s = env.compute_success(ag, dg).cpu().numpy()
+        assert np.array_equal(s, golden["success"])
+        her = env.compute_reward(torch.from_numpy(golden["her_ag"]).cuda(), torch.from_numpy(golden["her_dg"]).cuda())
+        assert her.shape == (32, 32)
+        assert np.array_equal(her.cpu().numpy().view(np.uint32), golden[f"her_reward_{reward_type}"].view(np.uint32))
+
+
+# ------------------------------------------------------------ physics parity
+def _oracle_ik_batch(cfg, snap, link, pos, orn):
+    out = []
+    for i in range(snap["f"].shape[1]):
+        out.append(O.inverse_kinematics(cfg, snap["f"][:9, i], link, pos[i], orn[i]))
+    return np.array(out)
+
+
+@pytest.mark.parametrize("task", ["reach", "push"])
+def test_ik_parity(ps, task):
+    """calculateInverseKinematics: GPU fp32 vs oracle fp64 from the same joints.
+
+    The DLS loop stops once |p - p*| <= 1e-4, so the two precisions may stop
+    one iteration apart; targets then still agree to ~1e-3 rad."""
+    B = 256
+    env = make_env(ps, task, "ee", B)
+    env.autoreset = False
+    env.reset(seed=5)
+    rng = np.random.default_rng(3)
+    for _ in range(3):
+        env.step(torch.from_numpy(rng.uniform(-1, 1, size=(B, 3)).astype(np.float32)).cuda())
+    cfg = oracle_config_for(env.sim.cfg)
+    snap = snapshot(env.sim)
+    ee = env.sim.get_link_position("panda", 11).cpu().numpy()
+    target = ee + rng.uniform(-0.05, 0.05, size=(B, 3))
+    orn = np.tile([1.0, 0.0, 0.0, 0.0], (B, 1))
+    q_gpu = env.sim.inverse_kinematics("panda", 11, target, orn).cpu().numpy()
+    q_ref = _oracle_ik_batch(cfg, snap, 11, target, orn)
+    err = np.abs(q_gpu - q_ref).max(axis=1)
+    assert np.median(err) < 1e-5
+    assert np.all(err < 2e-3)
+
+
+@pytest.mark.parametrize("task", ["reach", "push", "pick_and_place"])
+def test_sim_step_parity_same_motors(ps, task):
+    """Engine step (20 substeps) from identical joints, motors and object."""
+    B = 128
+    env = make_env(ps, task, "ee", B)
+    env.autoreset = False
+    env.reset(seed=21)
+    cfg = oracle_config_for(env.sim.cfg)
+    rng = np.random.default_rng(5)
+    worst_q = worst_qd = 0.0
+    for s in range(8):
+        env.step(torch.from_numpy(rng.uniform(-1, 1, size=(B, env.action_dim)).astype(np.float32)).cuda())
+        snap = snapshot(env.sim)  # motors hold the targets of this step's set_action
+        env.sim.step()
+        after = snapshot(env.sim)
+        for i in range(0, B, 4):
+            e = oracle_env_from(cfg, snap, i)
+            O.sim_step(cfg, e)
+            q_g, qd_g = after["f"][0:9, i], after["f"][9:18, i]
+            worst_q = max(worst_q, np.abs(q_g - np.array(e.q)).max())
+            worst_qd = max(worst_qd, np.abs(qd_g - np.array(e.qd)).max())
+            if task != "reach":
+                assert np.allclose(after["f"][63:66, i], np.array(e.cpos), atol=5e-4), (s, i)
+    assert worst_q < 2e-4, worst_q
+    assert worst_qd < 5e-3, worst_qd
+
+
+# Per-component tolerances of the fused env step (fp32 GPU vs fp64 oracle from
+# the same state).  Reach/Push measure ~1e-6 m / ~1e-4 m/s and are held tight.
+# PickAndPlace is ill-conditioned in the model itself: the fp64 oracle moves its
+# ee position by 8e-4, ee velocity by 3e-2 and finger width by 3.4e-3 under
+# fp32-ulp-sized state perturbations (test_oracle.py::
+# test_pick_and_place_conditioning), so its bounds are ~3x that conditioning.
+TOL = {
+    "reach": dict(ee_pos=2e-5, ee_vel=2e-3),
+    "push": dict(ee_pos=2e-5, ee_vel=2e-3, obj_pos=2e-5, obj_rot=1e-4, obj_vel=1e-4, obj_avel=2e-3),
+    "pick_and_place": dict(ee_pos=3e-3, ee_vel=1e-1, width=1e-2, obj_pos=1e-3, obj_rot=5e-3, obj_vel=5e-2,
+                           obj_avel=2e-1),
+}
+
+
+def _groups(obs_dim):
+    g = {"ee_pos": [0, 1, 2], "ee_vel": [3, 4, 5]}
+    k = 6
+    if obs_dim in (7, 19):
+        g["width"] = [6]
+        k = 7
+    if obs_dim > 7:
+        g.update(obj_pos=[k, k + 1, k + 2], obj_rot=[k + 3, k + 4, k + 5], obj_vel=[k + 6, k + 7, k + 8],
+                 obj_avel=[k + 9, k + 10, k + 11])
+    return g
+
+
+@pytest.mark.parametrize("task,control", TASKS)
+def test_env_step_parity_teacher_forced(ps, task, control):
+    """Each fused GPU env step vs one oracle env step from the same state."""
+    B, steps = 64, 10
+    env = make_env(ps, task, control, B)
+    env.autoreset = False
+    env.reset(seed=12345)
+    cfg = oracle_config_for(env.sim.cfg)
+    rng = np.random.default_rng(7)
+    groups = _groups(env.obs_dim)
+    worst = {k: 0.0 for k in groups}
+    flag_mismatch = 0
+    for s in range(steps):
+        snap = snapshot(env.sim)
+        a = rng.uniform(-1, 1, size=(B, env.action_dim)).astype(np.float32)
+        obs, r, te, tr, _ = env.step(torch.from_numpy(a).cuda())
+        og, te, tr = obs["observation"].cpu().numpy(), te.cpu().numpy(), tr.cpu().numpy()
+        for i in range(B):
+            o, ag, dg, rr, t_e, t_r = O.step(cfg, oracle_env_from(cfg, snap, i), a[i])
+            for k, idx in groups.items():
+                worst[k] = max(worst[k], float(np.abs(og[i, idx] - o[idx]).max()))
+            assert t_r == bool(tr[i])
+            flag_mismatch += t_e != bool(te[i])
+    print(task, control, {k: f"{v:.2e}" for k, v in worst.items()})
+    for k, v in worst.items():
+        assert v <= TOL[task][k], (k, v)
+    assert flag_mismatch <= 2
+
+
+def test_reach_free_running_parity(ps):
+    """Contact-free Reach, joint control (no IK stopping rule): 30 steps free-running."""
+    B = 16
+    env = make_env(ps, "reach", "joints", B)
+    env.autoreset = False
+    env.reset(seed=3)
+    cfg = oracle_config_for(env.sim.cfg)
+    snap = snapshot(env.sim)
+    oenvs = [oracle_env_from(cfg, snap, i) for i in range(B)]
+    rng = np.random.default_rng(11)
+    for s in range(30):
+        a = rng.uniform(-1, 1, size=(B, 7)).astype(np.float32)
+        obs, *_ = env.step(torch.from_numpy(a).cuda())
+        og = obs["observation"].cpu().numpy()
+        for i in range(B):
+            o, *_ = O.step(cfg, oenvs[i], a[i])
+            assert np.allclose(og[i, :3], o[:3], atol=1e-3), (s, i)
+            assert np.allclose(og[i, 3:], o[3:], atol=2e-2), (s, i)
+
+
+@pytest.mark.parametrize("task", ["reach", "push", "pick_and_place"])
+def test_autoreset_continues_generator(ps, task):
+    """Every in-kernel reset (success or TimeLimit) draws the next goal/object
+    from the env's own PCG64 stream: after n resets the goal equals the
+    oracle's n-th unseeded reset after reset(seed) -- bit-exact."""
+    B = 32
+    env = make_env(ps, task, "ee", B)
+    env.reset(seed=100)
+    cfg = oracle_config_for(env.sim.cfg)
+    zeros = torch.zeros(B, env.action_dim, device="cuda")
+    n_resets = np.zeros(B, int)
+    for s in range(60):
+        obs, r, te, tr, info = env.step(zeros)
+        n_resets += (te | tr).cpu().numpy().astype(int)
+    assert (n_resets >= 1).all()
+    goal = env.sim.goal[:, :B].t().cpu().numpy()
+    for i in range(B):
+        e = O.new_env(cfg)
+        O.reset(cfg, e, seed=100 + i)
+        for _ in range(n_resets[i]):
+            O.reset(cfg, e, seed=None)
+        assert np.array_equal(goal[i], np.array(e.goal))
+
+
+def test_determinism_and_save_restore(ps):
+    B = 128
+    a = torch.rand(6, B, 3, device="cuda") * 2 - 1
+    outs = []
+    for _ in range(2):
+        env = make_env(ps, "push", "ee", B)
+        env.reset(seed=6789)
+        for k in range(6):
+            obs, *_ = env.step(a[k])
+        outs.append(obs["observation"].cpu())
+    assert torch.equal(outs[0], outs[1])
+    env = make_env(ps, "reach", "ee", B)
+    env.reset(seed=1)
+    sid = env.save_state()
+    o1, *_ = env.step(a[0])
+    env.reset(seed=2)
+    env.restore_state(sid)
+    o2, *_ = env.step(a[0])
+    for k in o1:
+        assert torch.equal(o1[k], o2[k])
+    env.remove_state(sid)
+    with pytest.raises(Exception):
+        env.restore_state(sid)
+
+
+@pytest.mark.parametrize("task", ["push", "pick_and_place"])
+def test_large_batch_properties(ps, task):
+    """At the bench size: finite, bounded observations and exact TimeLimit."""
+    B = 65536
+    env = make_env(ps, task, "ee", B)
+    env.reset(seed=12345)
+    for s in range(5):
+        obs, r, te, tr, _ = env.step(torch.rand(B, env.action_dim, device="cuda") * 2 - 1)
+    o = obs["observation"]
+    assert torch.isfinite(o).all()
+    # a gripper strike can spin the 4 cm cube to tens of rad/s (the oracle
+    # reproduces these states: DESIGN.md §Parity); everything stays physical
+    assert (o.abs() < 100).all()
+    assert (env.sim.get_base_position("object")[:, 2] > -0.45).all()
+    assert not tr.any()
+    assert int(env.sim.elapsed[:B].max()) <= 5 and int(env.sim.elapsed[:B].min()) >= 0
