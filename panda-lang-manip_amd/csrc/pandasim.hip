@@ -98,6 +98,26 @@ PS_D void store_motors(const StateView &s, int64_t i, const Motors &m) {
         s.F(PS_F_MIMP + d, i) = m.imp[d];
     }
 }
+
+// The motor rows' targets/gains are constant over a control step: they are
+// re-read from the (L2-resident) state buffer at every substep instead of
+// occupying 45 registers through the solver.  The index goes through an empty
+// asm so the loads cannot be hoisted out of the substep loop.
+template <bool HAS_CUBE, bool STD_MOTORS>
+PS_D void run_substeps(const KParams &P, int64_t i, int n, float q[9], float qd[9], Cube &cb, const MJStore &lds) {
+    for (int st = 0; st < n; st++) {
+        int64_t ii = i;
+        asm volatile("" : "+v"(ii));
+        Motors m;
+        if constexpr (STD_MOTORS) {
+#pragma unroll
+            for (int d = 0; d < 9; d++) m.target[d] = P.s.F(PS_F_MTARGET + d, ii);
+        } else {
+            load_motors(P.s, ii, m);
+        }
+        substep<HAS_CUBE, STD_MOTORS>(P.sc, q, qd, m, cb, lds);
+    }
+}
 PS_D void load_cube(const StateView &s, int64_t i, Cube &c) {
     c.pos = mk(s.F(PS_F_CPOS, i), s.F(PS_F_CPOS + 1, i), s.F(PS_F_CPOS + 2, i));
     c.quat = Q4{s.F(PS_F_CQUAT, i), s.F(PS_F_CQUAT + 1, i), s.F(PS_F_CQUAT + 2, i), s.F(PS_F_CQUAT + 3, i)};
@@ -207,7 +227,11 @@ PS_D void set_action(const KParams &P, const float *act, const float q[9], Motor
         V3 t = p + mk(a[0] * 0.05f, a[1] * 0.05f, a[2] * 0.05f);
         t.z = fmaxf(0.0f, t.z);
         float qik[9];
+#ifndef PS_DBG_NO_IK
         inverse_kinematics<11>(q, t - P.sc.base, Q4{1.0f, 0.0f, 0.0f, 0.0f}, qik);
+#else
+        for (int d = 0; d < 9; d++) qik[d] = q[d] + t.x;
+#endif
 #pragma unroll
         for (int d = 0; d < 7; d++) tq[d] = qik[d];
     } else {
@@ -277,9 +301,14 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
     load_robot(s, i, q, qd);
     Cube cb;
     if constexpr (HAS_CUBE) load_cube(s, i, cb);
-    Motors m;
-    set_action<CONTROL>(P, actions + i * P.action_dim, q, m);
-    for (int st = 0; st < PM_SUBSTEPS; st++) substep<HAS_CUBE>(P.sc, q, qd, m, cb);
+    {
+        Motors m;
+        set_action<CONTROL>(P, actions + i * P.action_dim, q, m);
+        store_motors(s, i, m);
+    }
+    __shared__ float smem[LDS_FLOATS * kBlock];
+    MJStore lds{(lds_float *)(smem + threadIdx.x), kBlock};
+    run_substeps<HAS_CUBE, true>(P, i, PM_SUBSTEPS, q, qd, cb, lds);
     double g[3] = {s.goal[i], s.goal[s.stride + i], s.goal[2 * s.stride + i]};
     // obs of the stepped state
     float a0, a1, a2;
@@ -309,7 +338,6 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
     }
     s.elapsed[i] = el;
     store_robot(s, i, q, qd);
-    store_motors(s, i, m);
     if constexpr (HAS_CUBE) store_cube(s, i, cb);
     write_obs<TASK>(P, i, q, qd, cb, g, obs, ag, dg);
 }
@@ -323,9 +351,9 @@ __global__ __launch_bounds__(kBlock) void k_sim_step(KParams P, int n_substeps) 
     load_robot(s, i, q, qd);
     Cube cb;
     if constexpr (HAS_CUBE) load_cube(s, i, cb);
-    Motors m;
-    load_motors(s, i, m);
-    for (int st = 0; st < n_substeps; st++) substep<HAS_CUBE>(P.sc, q, qd, m, cb);
+    __shared__ float smem[LDS_FLOATS * kBlock];
+    MJStore lds{(lds_float *)(smem + threadIdx.x), kBlock};
+    run_substeps<HAS_CUBE, false>(P, i, n_substeps, q, qd, cb, lds);
     store_robot(s, i, q, qd);
     if constexpr (HAS_CUBE) store_cube(s, i, cb);
 }

@@ -41,6 +41,8 @@ PS_D Frame child_frame(const Frame &P, float q) {
                               P.R.m[r * 3 + 2] * (float)Ro.m[2 * 3 + c];
     V3 oj = P.o + mul(P.R, mk((float)d.o[0], (float)d.o[1], (float)d.o[2]));
     if constexpr (d.type == PM_JOINT_REVOLUTE) {
+        // libm sincosf (its range-reduction branch doubles as a scheduling
+        // fence; __sinf/__cosf measured 12% slower on Push through spills)
         float s, c;
         sincosf(q, &s, &c);
 #pragma unroll
@@ -160,15 +162,17 @@ PS_D void mass_matrix(const Kin &k, float M[45]) {
 // pass over the chain; every link force/moment is folded into prefix sums so
 // tau_i = a_i . ((N_tot - N_pre_i) - o_i x (F_tot - F_pre_i)) with moments
 // about the base origin.
+// Frames are produced on the fly (FK fused into the forward sweep) so no
+// 12-frame kinematics array is held live next to the dynamics.
 template <int I>
-PS_D void link_wrench(const Kin &k, V3 w, V3 dw, V3 vo, V3 ao, V3 &F, V3 &N) {
+PS_D void link_wrench_f(const Frame &f, V3 w, V3 dw, V3 vo, V3 ao, V3 &F, V3 &N) {
     constexpr LinkDef d = link_def(I);
     constexpr float m = (float)d.mass;
-    V3 c = com_pos<I>(k);
-    V3 rc = c - k.f[I].o;
+    V3 c = f.o + mul(f.R, mk((float)d.com[0], (float)d.com[1], (float)d.com[2]));
+    V3 rc = c - f.o;
     V3 vc = vo + cross(w, rc);
     V3 ac = ao + cross(dw, rc) + cross(w, cross(w, rc));
-    S3 Iw = rotate_diag(k.f[I].R, (float)link_inertia(I, 0), (float)link_inertia(I, 1), (float)link_inertia(I, 2));
+    S3 Iw = rotate_diag(f.R, (float)link_inertia(I, 0), (float)link_inertia(I, 1), (float)link_inertia(I, 2));
     V3 Iww = mul(Iw, w);
     float cl = (float)PM_LINEAR_DAMPING + (float)PM_LINEAR_DAMPING * norm(vc);
     float ca = (float)PM_ANGULAR_DAMPING + (float)PM_ANGULAR_DAMPING * norm(w);
@@ -177,36 +181,42 @@ PS_D void link_wrench(const Kin &k, V3 w, V3 dw, V3 vo, V3 ao, V3 &F, V3 &N) {
     N = Nc + cross(c, F);  // about the base origin
 }
 
-PS_D void bias_forces(const Kin &k, const float qd[9], float h[9]) {
+PS_D void bias_forces(const float q[9], const float qd[9], float h[9]) {
     V3 w = mk(0, 0, 0), dw = mk(0, 0, 0), vo = mk(0, 0, 0), ao = mk(0, 0, -(float)PM_GRAVITY_Z);
-    V3 prev_o = mk(0, 0, 0);
-    V3 Fpre[7], Npre[7];
+    Frame f;
+    f.R = M3{{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+    f.o = mk(0, 0, 0);
+    V3 prev_o = f.o;
+    V3 Fpre[7], Npre[7], ax[7], org[7];
     V3 Fs = mk(0, 0, 0), Ns = mk(0, 0, 0);
-    V3 ax[7];
     static_for<0, 7>([&](auto II) {
         constexpr int I = decltype(II)::value;
-        V3 r = k.f[I].o - prev_o;
+        f = child_frame<I>(f, q[I]);
+        V3 r = f.o - prev_o;
         vo = vo + cross(w, r);
         ao = ao + cross(dw, r) + cross(w, cross(w, r));
-        V3 a = col(k.f[I].R, 2);
+        V3 a = col(f.R, 2);
         ax[I] = a;
+        org[I] = f.o;
         dw = dw + cross(w, a) * qd[I];
         w = w + a * qd[I];
         Fpre[I] = Fs;
         Npre[I] = Ns;
         V3 F, N;
-        link_wrench<I>(k, w, dw, vo, ao, F, N);
+        link_wrench_f<I>(f, w, dw, vo, ao, F, N);
         Fs = Fs + F;
         Ns = Ns + N;
-        prev_o = k.f[I].o;
+        prev_o = f.o;
     });
-    // link 7 (massless, fixed) and hand (8): same frame origin as link 7
+    // link 7 (massless, fixed) and the hand (8): same origin as link 7
+    f = child_frame<7>(f, 0.0f);
+    f = child_frame<8>(f, 0.0f);
     {
-        V3 r = k.f[8].o - prev_o;
+        V3 r = f.o - prev_o;
         vo = vo + cross(w, r);
         ao = ao + cross(dw, r) + cross(w, cross(w, r));
         V3 F, N;
-        link_wrench<8>(k, w, dw, vo, ao, F, N);
+        link_wrench_f<8>(f, w, dw, vo, ao, F, N);
         Fs = Fs + F;
         Ns = Ns + N;
     }
@@ -214,22 +224,24 @@ PS_D void bias_forces(const Kin &k, const float qd[9], float h[9]) {
     static_for<0, 2>([&](auto JJ) {
         constexpr int J = decltype(JJ)::value;
         constexpr int L = 9 + J;
-        V3 a = dof_axis<7 + J>(k);
+        Frame ff = child_frame<L>(f, q[7 + J]);
+        constexpr LinkDef ld = link_def(L);
+        V3 a = mul(ff.R, mk((float)ld.axis[0], (float)ld.axis[1], (float)ld.axis[2]));
         float v = qd[7 + J];
-        V3 r = k.f[L].o - k.f[8].o;
+        V3 r = ff.o - f.o;
         V3 vf = vo + cross(w, r) + a * v;
         V3 af = ao + cross(dw, r) + cross(w, cross(w, r)) + cross(w, a) * (2.0f * v);
         V3 F, N;
-        link_wrench<L>(k, w, dw, vf, af, F, N);
+        link_wrench_f<L>(ff, w, dw, vf, af, F, N);
         h[7 + J] = dot(a, F);
         Fs = Fs + F;
         Ns = Ns + N;
     });
-    static_for<0, 7>([&](auto II) {
-        constexpr int I = decltype(II)::value;
+#pragma unroll
+    for (int I = 0; I < 7; I++) {
         V3 Fsub = Fs - Fpre[I], Nsub = Ns - Npre[I];
-        h[I] = dot(ax[I], Nsub - cross(k.f[I].o, Fsub));
-    });
+        h[I] = dot(ax[I], Nsub - cross(org[I], Fsub));
+    }
 }
 
 // M = L L^T, then M^-1 (packed symmetric) = L^-T L^-1
@@ -410,6 +422,11 @@ PS_D void plane_space(V3 n, V3 &p, V3 &q) {
 
 constexpr int NG = PM_MAX_GROUND_CONTACTS;
 constexpr int NR = PM_MAX_ROBOT_CONTACTS;
+// LDS floats per lane: M^-1 J^T of the 3 rows of every gripper contact, then
+// the packed M^-1 (read by the joint rows).  153 floats x 256 lanes per CU =
+// 153 KiB of the 160 KiB LDS at one wave per SIMD.
+constexpr int LDS_MI_OFFSET = NR * 27;
+constexpr int LDS_FLOATS = LDS_MI_OFFSET + 45;
 
 // cube-ground contact: cube-only rows; normal +z, friction dirs of planeSpace(+z) = (0,-1,0), (1,0,0)
 struct GroundContact {
@@ -417,18 +434,29 @@ struct GroundContact {
     float rhs[3], lam[3], dinv[3];
 };
 
-// gripper contact: robot rows with explicit Jacobians; optional cube side
+// gripper contact: robot rows with explicit Jacobians (M^-1 J^T lives in LDS)
 struct RobotContact {
-    float J[3][9], MJ[3][9];
+    float J[3][9];
     V3 dir[3];
-    V3 rB;  // cube side: point on cube - cube COM (valid if on_cube)
+    V3 rn[3];  // cube side: (pB - x_cube) x dir (zero when the contact is with the ground)
     float rhs[3], lam[3], dinv[3], mu;
-    bool on_cube;
 };
 
-struct Solver {
-    float dv[9];
-    V3 dw, dvl;  // cube angular / linear velocity deltas
+// per-lane view of the LDS rows: element (slot, row, k) at base[((slot*3 + row)*9 + k) * stride]
+typedef __attribute__((address_space(3))) float lds_float;
+struct MJStore {
+    lds_float *base;
+    int stride;
+    PS_D lds_float &at(int slot, int row, int k) const { return base[((slot * 3 + row) * 9 + k) * stride]; }
+    PS_D lds_float &mi(int k) const { return base[(LDS_MI_OFFSET + k) * stride]; }
+    // a copy whose address the compiler cannot see through: loads from it are
+    // not loop-invariant, so they stay in the PGS loop as ds_reads instead of
+    // being hoisted into (spilled) registers
+    PS_D MJStore opaque() const {
+        MJStore r = *this;
+        asm volatile("" : "+v"(r.base));
+        return r;
+    }
 };
 
 PS_D float jrow_dot(const float J[9], const float v[9]) {
@@ -438,18 +466,52 @@ PS_D float jrow_dot(const float J[9], const float v[9]) {
     return s;
 }
 
+// Geometry that outlives the kinematics: DoF axes/origins (gripper-contact
+// Jacobians) and world sphere centres.
+struct Geo {
+    V3 ax[9], org[7], spw[PM_NUM_SPHERES];
+};
+
 // ----------------------------------------------------------------- substep
 // One btMultiBodyDynamicsWorld::stepSimulation(1/500 s): see the oracle's
 // po_substep for the row-by-row restatement this mirrors.
-template <bool HAS_CUBE>
-PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cube &cb) {
+// PGS residual of a row is dl / dinv (the impulse change in velocity units).
+// v_rcp_f32 replaces the IEEE division; a zero dinv gives 0 * inf = NaN, which
+// fmaxf() in the residual max ignores, matching the reference's skip.
+PS_D float res_scale(float dinv) { return __builtin_amdgcn_rcpf(dinv); }
+
+// STD_MOTORS: the motors are the ones RobotTaskEnv.step sets (POSITION_CONTROL
+// on all nine joints with the fixed Panda gains and forces, panda.py:40-56), so
+// only the targets are per-env; otherwise every gain comes from `mt`.
+template <bool HAS_CUBE, bool STD_MOTORS>
+PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cube &cb, const MJStore &lds) {
     const float dt = (float)PM_TIMESTEP;
-    Kin k;
-    fk(q, k);
     float Mi[45], hb[9];
-    mass_matrix(k, Mi);
-    bias_forces(k, qd, hb);
+    Geo geo;
+    // phases are fenced so the scheduler does not interleave them (each one's
+    // transient state is large; overlapping them is what spilled to scratch)
+    bias_forces(q, qd, hb);
+    __builtin_amdgcn_sched_barrier(0);
+    {
+        Kin k;
+        fk(q, k);
+        static_for<0, 9>([&](auto D) {
+            constexpr int d = decltype(D)::value;
+            geo.ax[d] = dof_axis<d>(k);
+            if constexpr (d < 7) geo.org[d] = k.f[d].o;
+        });
+        static_for<0, PM_NUM_SPHERES>([&](auto SS) {
+            constexpr int S = decltype(SS)::value;
+            constexpr SphereDef s = sphere_def(S);
+            geo.spw[S] = k.f[s.link].o + mul(k.f[s.link].R, mk((float)s.c[0], (float)s.c[1], (float)s.c[2])) + sc.base;
+        });
+        mass_matrix(k, Mi);
+    }
+    __builtin_amdgcn_sched_barrier(0);
     spd_inverse(Mi);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < 45; k++) lds.mi(k) = Mi[k];
     float v1[9];
 #pragma unroll
     for (int a = 0; a < 9; a++) {
@@ -471,10 +533,12 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
         cw1 = cb.omg - cb.omg * (ca * dt);
     }
 
-    // ---- joint-space rows: limits (lower/upper) and motors
+    // ---- joint-space rows: limits and motors.  A joint can be beyond at most
+    // one of its limits, so each joint carries one limit row whose side is a
+    // bit of lim_up; rows that are off have bounds [0, 0] and are exact no-ops.
     float dinvj[9];
-    float lim_rhs[9][2], lim_lam[9][2];
-    bool lim_on[9][2];
+    float lim_rhs[9], lim_lam[9];
+    unsigned lim_on = 0u, lim_up = 0u;
     float split_dq[9];
     float mot_rhs[9], mot_lam[9];
 #pragma unroll
@@ -482,26 +546,35 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
         float den = Mi[sidx(d, d)];
         dinvj[d] = den > 2.2204460492503131e-16f ? 1.0f / den : 0.0f;
         split_dq[d] = 0.0f;
+        lim_rhs[d] = 0.0f;
+        lim_lam[d] = 0.0f;
 #pragma unroll
         for (int side = 0; side < 2; side++) {
             float lo = (float)dof_def(d).lo, hi = (float)dof_def(d).hi;
             float pen = side ? hi - q[d] : q[d] - lo;
             float sgn = side ? -1.0f : 1.0f;
-            lim_on[d][side] = pen <= 0.0f;
+            bool on = pen <= 0.0f;
             float velerr = -sgn * v1[d];
             bool combined = pen > (float)PM_SPLIT_PENETRATION_THRESHOLD;
             float poserr = -pen * (float)PM_ERP / dt;
-            lim_rhs[d][side] = (combined ? poserr + velerr : velerr) * dinvj[d];
-            lim_lam[d][side] = 0.0f;
-            if (lim_on[d][side] && !combined) split_dq[d] += sgn * (-pen) * (float)PM_SPLIT_LIMIT_ERP;
+            if (on) {
+                lim_on |= 1u << d;
+                lim_up |= side ? 1u << d : 0u;
+                lim_rhs[d] = (combined ? poserr + velerr : velerr) * dinvj[d];
+                if (!combined) split_dq[d] += sgn * (-pen) * (float)PM_SPLIT_LIMIT_ERP;
+            }
         }
-        float target = mt.kp[d] * (mt.target[d] - q[d]) / dt + v1[d] + mt.kd[d] * (mt.vel[d] - v1[d]);
+        float kp = STD_MOTORS ? (float)PM_MOTOR_KP : mt.kp[d], kd = STD_MOTORS ? (float)PM_MOTOR_KD : mt.kd[d];
+        float vel = STD_MOTORS ? 0.0f : mt.vel[d];
+        float target = kp * (mt.target[d] - q[d]) / dt + v1[d] + kd * (vel - v1[d]);
         mot_rhs[d] = (target - v1[d]) * dinvj[d];
         mot_lam[d] = 0.0f;
     }
 
     // ---- contacts
     GroundContact gc[NG];
+#pragma unroll
+    for (int s = 0; s < NG; s++) gc[s] = GroundContact{mk(0, 0, 0), {0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
     int ng = 0;
     RobotContact rc[NR];
     int nr = 0;
@@ -549,96 +622,55 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
         }
     }
     {
-        // gripper spheres (base-relative frames -> world)
-        V3 spw[PM_NUM_SPHERES];
-        static_for<0, PM_NUM_SPHERES>([&](auto SS) {
-            constexpr int S = decltype(SS)::value;
-            constexpr SphereDef s = sphere_def(S);
-            spw[S] = k.f[s.link].o + mul(k.f[s.link].R, mk((float)s.c[0], (float)s.c[1], (float)s.c[2])) + sc.base;
-        });
-        auto add_robot = [&](int link, V3 pA, V3 n, float dist, float mu, bool on_cube, V3 pB) {
-            RobotContact c;
-            plane_space(n, c.dir[1], c.dir[2]);
-            c.dir[0] = n;
-            c.on_cube = on_cube;
-            c.rB = pB - cb.pos;
-            c.mu = mu;
-            V3 p = pA - sc.base;
+        // 1) candidate gripper contacts in spec order (spheres vs cube, then
+        //    spheres vs ground) -> small records; the first NR active ones
+        //    are assigned slots 0..NR-1 (select into compile-time slots)
+        struct Cand {
+            V3 pA, pB, n;
+            float dist, mu;
+            int link;
+            bool on_cube;
+        };
+        Cand slot[NR];
 #pragma unroll
-            for (int j = 0; j < 3; j++) {
-                V3 dj = c.dir[j];
-                static_for<0, 7>([&](auto DD) {
-                    constexpr int D = decltype(DD)::value;
-                    V3 a = col(k.f[D].R, 2);
-                    c.J[j][D] = dot(a, cross(p - k.f[D].o, dj));
-                });
-                c.J[j][7] = link == 9 ? dot(dof_axis<7>(k), dj) : 0.0f;
-                c.J[j][8] = link == 10 ? dot(dof_axis<8>(k), dj) : 0.0f;
-#pragma unroll
-                for (int a = 0; a < 9; a++) {
-                    float s = 0.0f;
-#pragma unroll
-                    for (int b = 0; b < 9; b++) s += Mi[sidx(a, b)] * c.J[j][b];
-                    c.MJ[j][a] = s;
-                }
-                float den = jrow_dot(c.J[j], c.MJ[j]);
-                float rel = jrow_dot(c.J[j], v1);
-                if (on_cube) {
-                    V3 rn = cross(c.rB, dj);
-                    den += dot(rn, rn) * inv_I + dot(dj, dj) * inv_m;
-                    rel -= dot(rn, cw1) + dot(dj, cv1);
-                }
-                c.dinv[j] = den > 2.2204460492503131e-16f ? 1.0f / den : 0.0f;
-                c.lam[j] = 0.0f;
-                if (j == 0) {
-                    float pen = dist + (float)PM_LINEAR_SLOP;
-                    float velerr = -rel, poserr = 0.0f;
-                    if (pen > 0.0f) velerr -= pen / dt;
-                    else poserr = -pen * (float)PM_ERP / dt;
-                    bool combined = pen > (float)PM_SPLIT_PENETRATION_THRESHOLD;
-                    c.rhs[0] = (combined ? poserr + velerr : velerr) * c.dinv[0];
-                } else {
-                    c.rhs[j] = -rel * c.dinv[j];
-                }
-            }
+        for (int s = 0; s < NR; s++) slot[s] = Cand{mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 1), 1.0f, 0.0f, 8, false};
+        auto offer = [&](const Cand &c) {
 #pragma unroll
             for (int s = 0; s < NR; s++)
-                if (s == nr) rc[s] = c;
+                if (s == nr) slot[s] = c;
             nr++;
         };
+#ifndef PS_DBG_NO_RC
         if constexpr (HAS_CUBE) {
             const float h = sc.half;
             static_for<0, PM_NUM_SPHERES>([&](auto SS) {
                 constexpr int S = decltype(SS)::value;
                 constexpr SphereDef s = sphere_def(S);
-                if (nr < NR) {
-                    V3 loc = tmul(Rc, spw[S] - cb.pos);
-                    V3 cl = mk(fminf(fmaxf(loc.x, -h), h), fminf(fmaxf(loc.y, -h), h), fminf(fmaxf(loc.z, -h), h));
-                    V3 dif = loc - cl;
-                    float dn = norm(dif);
-                    V3 nl;
-                    float dist;
-                    if (dn > 1e-9f) {
-                        nl = dif * (1.0f / dn);
-                        dist = dn - (float)s.r;
-                    } else {
-                        float bx = h - fabsf(loc.x), by = h - fabsf(loc.y), bz = h - fabsf(loc.z);
-                        int ax = 0;
-                        float best = bx;
-                        if (by < best) { best = by; ax = 1; }
-                        if (bz < best) { best = bz; ax = 2; }
-                        float sg;
-                        if (ax == 0) { sg = loc.x >= 0.0f ? 1.0f : -1.0f; nl = mk(sg, 0, 0); cl.x = sg * h; }
-                        else if (ax == 1) { sg = loc.y >= 0.0f ? 1.0f : -1.0f; nl = mk(0, sg, 0); cl.y = sg * h; }
-                        else { sg = loc.z >= 0.0f ? 1.0f : -1.0f; nl = mk(0, 0, sg); cl.z = sg * h; }
-                        dist = -best - (float)s.r;
-                    }
-                    if (dist < (float)PM_CONTACT_MARGIN_SPHERE) {
-                        V3 n = mul(Rc, nl);
-                        V3 pB = cb.pos + mul(Rc, cl);
-                        V3 pA = spw[S] - n * (float)s.r;
-                        add_robot(s.link, pA, n, dist, (float)(s.mu * PM_DEFAULT_FRICTION), true, pB);
-                    }
+                V3 loc = tmul(Rc, geo.spw[S] - cb.pos);
+                V3 cl = mk(fminf(fmaxf(loc.x, -h), h), fminf(fmaxf(loc.y, -h), h), fminf(fmaxf(loc.z, -h), h));
+                V3 dif = loc - cl;
+                float dn = norm(dif);
+                V3 nl;
+                float dist;
+                if (dn > 1e-9f) {
+                    nl = dif * (1.0f / dn);
+                    dist = dn - (float)s.r;
+                } else {
+                    float bx = h - fabsf(loc.x), by = h - fabsf(loc.y), bz = h - fabsf(loc.z);
+                    int ax = 0;
+                    float best = bx;
+                    if (by < best) { best = by; ax = 1; }
+                    if (bz < best) { best = bz; ax = 2; }
+                    float sg;
+                    if (ax == 0) { sg = loc.x >= 0.0f ? 1.0f : -1.0f; nl = mk(sg, 0, 0); cl.x = sg * h; }
+                    else if (ax == 1) { sg = loc.y >= 0.0f ? 1.0f : -1.0f; nl = mk(0, sg, 0); cl.y = sg * h; }
+                    else { sg = loc.z >= 0.0f ? 1.0f : -1.0f; nl = mk(0, 0, sg); cl.z = sg * h; }
+                    dist = -best - (float)s.r;
+                }
+                if (nr < NR && dist < (float)PM_CONTACT_MARGIN_SPHERE) {
+                    V3 n = mul(Rc, nl);
+                    offer(Cand{geo.spw[S] - n * (float)s.r, cb.pos + mul(Rc, cl), n, dist,
+                               (float)(s.mu * PM_DEFAULT_FRICTION), s.link, true});
                 }
             });
         }
@@ -646,190 +678,253 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
             constexpr int S = decltype(SS)::value;
             constexpr SphereDef s = sphere_def(S);
             float top;
-            if (nr < NR && ground_top(sc, spw[S].x, spw[S].y, top)) {
-                float dist = spw[S].z - (float)s.r - top;
+            if (nr < NR && ground_top(sc, geo.spw[S].x, geo.spw[S].y, top)) {
+                float dist = geo.spw[S].z - (float)s.r - top;
                 if (dist < (float)PM_CONTACT_MARGIN_SPHERE) {
-                    V3 pA = spw[S] - mk(0, 0, (float)s.r);
-                    add_robot(s.link, pA, mk(0, 0, 1), dist, (float)(s.mu * PM_DEFAULT_FRICTION), false, pA);
+                    V3 pA = geo.spw[S] - mk(0, 0, (float)s.r);
+                    offer(Cand{pA, pA, mk(0, 0, 1), dist, (float)(s.mu * PM_DEFAULT_FRICTION), s.link, false});
                 }
             }
         });
+#endif
+        // 2) rows of each used slot: J (registers), M^-1 J^T (LDS), rhs, bounds
+#pragma unroll
+        for (int sl = 0; sl < NR; sl++) {
+            if (sl < nr) {
+                const Cand &cd = slot[sl];
+                RobotContact &c = rc[sl];
+                V3 dirs[3];
+                dirs[0] = cd.n;
+                plane_space(cd.n, dirs[1], dirs[2]);
+                c.mu = cd.mu;
+                V3 p = cd.pA - sc.base;
+                V3 rB = cd.pB - cb.pos;
+#pragma unroll
+                for (int j = 0; j < 3; j++) {
+                    V3 dj = dirs[j];
+#pragma unroll
+                    for (int D = 0; D < 7; D++) c.J[j][D] = dot(geo.ax[D], cross(p - geo.org[D], dj));
+                    c.J[j][7] = cd.link == 9 ? dot(geo.ax[7], dj) : 0.0f;
+                    c.J[j][8] = cd.link == 10 ? dot(geo.ax[8], dj) : 0.0f;
+                    float den = 0.0f;
+#pragma unroll
+                    for (int a = 0; a < 9; a++) {
+                        float s = 0.0f;
+#pragma unroll
+                        for (int b = 0; b < 9; b++) s += Mi[sidx(a, b)] * c.J[j][b];
+                        lds.at(sl, j, a) = s;
+                        den += c.J[j][a] * s;
+                    }
+                    float rel = jrow_dot(c.J[j], v1);
+                    c.rn[j] = cd.on_cube ? cross(rB, dj) : mk(0, 0, 0);
+                    c.dir[j] = cd.on_cube ? dj : mk(0, 0, 0);  // cube side only
+                    if (cd.on_cube) {
+                        den += dot(c.rn[j], c.rn[j]) * inv_I + dot(dj, dj) * inv_m;
+                        rel -= dot(c.rn[j], cw1) + dot(dj, cv1);
+                    }
+                    c.dinv[j] = den > 2.2204460492503131e-16f ? 1.0f / den : 0.0f;
+                    c.lam[j] = 0.0f;
+                    if (j == 0) {
+                        float pen = cd.dist + (float)PM_LINEAR_SLOP;
+                        float velerr = -rel, poserr = 0.0f;
+                        if (pen > 0.0f) velerr -= pen / dt;
+                        else poserr = -pen * (float)PM_ERP / dt;
+                        bool combined = pen > (float)PM_SPLIT_PENETRATION_THRESHOLD;
+                        c.rhs[0] = (combined ? poserr + velerr : velerr) * c.dinv[0];
+                    } else {
+                        c.rhs[j] = -rel * c.dinv[j];
+                    }
+                }
+            } else {
+                // unused slot: all-zero rows (finite M^-1 J^T too) are no-ops in PGS
+                RobotContact &c = rc[sl];
+                c.mu = 0.0f;
+#pragma unroll
+                for (int j = 0; j < 3; j++) {
+#pragma unroll
+                    for (int a = 0; a < 9; a++) {
+                        c.J[j][a] = 0.0f;
+                        lds.at(sl, j, a) = 0.0f;
+                    }
+                    c.dir[j] = mk(0, 0, 0);
+                    c.rn[j] = mk(0, 0, 0);
+                    c.rhs[j] = c.lam[j] = c.dinv[j] = 0.0f;
+                }
+            }
+        }
     }
+    __builtin_amdgcn_sched_barrier(0);
 
     // ---- projected Gauss-Seidel
-    Solver S;
+    // Every row kind is gated by a wave-uniform ballot (a scalar branch: the
+    // block runs if any lane of the wave needs it); inside, lanes without the
+    // row hold all-zero data or [0, 0] bounds, which leave every impulse and
+    // velocity untouched, so no per-lane exec masking or phi copies remain.
+    float dv[9];
 #pragma unroll
-    for (int d = 0; d < 9; d++) S.dv[d] = 0.0f;
-    S.dw = mk(0, 0, 0);
-    S.dvl = mk(0, 0, 0);
+    for (int d = 0; d < 9; d++) dv[d] = 0.0f;
+    V3 dw = mk(0, 0, 0), dvl = mk(0, 0, 0);
+    float res;
+    MJStore L = lds;
 
-    auto joint_row = [&](int d, float sgn, float rhs, float &lam, float lo, float hi) -> float {
-        float dl = rhs - dinvj[d] * (sgn * S.dv[d]);
-        float sum = lam + dl;
-        if (sum < lo) { dl = lo - lam; lam = lo; }
-        else if (sum > hi) { dl = hi - lam; lam = hi; }
-        else lam = sum;
+    auto joint_row = [&](int d, float sgn, float rhs, float &lam, float lo, float hi) {
+        float dl = rhs - dinvj[d] * (sgn * dv[d]);
+        float nl = fminf(fmaxf(lam + dl, lo), hi);
+        dl = nl - lam;
+        lam = nl;
         float f = sgn * dl;
 #pragma unroll
-        for (int a = 0; a < 9; a++) S.dv[a] += Mi[sidx(a, d)] * f;
-        return dinvj[d] != 0.0f ? dl / dinvj[d] : 0.0f;
+        for (int a = 0; a < 9; a++) dv[a] += L.mi(sidx(a, d)) * f;
+        float x = dl * L.mi(sidx(d, d));  // residual dl / dinv = dl * (J M^-1 J^T)
+        res = fmaxf(res, x * x);
+    };
+    auto limit_row = [&](int d) {
+        if (__builtin_amdgcn_ballot_w64((lim_on >> d) & 1u)) {
+            float sgn = (lim_up >> d) & 1u ? -1.0f : 1.0f;
+            float hi = (lim_on >> d) & 1u ? (float)PM_LIMIT_MAX_IMPULSE : 0.0f;
+            joint_row(d, sgn, lim_rhs[d], lim_lam[d], 0.0f, hi);
+        }
+    };
+    auto motor_row = [&](int d) {
+        float imp = STD_MOTORS ? (float)(joint_force(d) * PM_TIMESTEP) : mt.imp[d];
+        joint_row(d, 1.0f, mot_rhs[d], mot_lam[d], -imp, imp);
     };
 
-    for (int it = 0; it < PM_SOLVER_ITERATIONS; it++) {
-        float res = 0.0f, x;
-        if (it & 1) {
-#pragma unroll
-            for (int d = 0; d < 9; d++)
-#pragma unroll
-                for (int side = 0; side < 2; side++)
-                    if (lim_on[d][side]) {
-                        x = joint_row(d, side ? -1.0f : 1.0f, lim_rhs[d][side], lim_lam[d][side], 0.0f,
-                                      (float)PM_LIMIT_MAX_IMPULSE);
-                        res = fmaxf(res, x * x);
-                    }
-#pragma unroll
-            for (int d = 0; d < 9; d++)
-                if (mt.imp[d] != 0.0f) {
-                    x = joint_row(d, 1.0f, mot_rhs[d], mot_lam[d], -mt.imp[d], mt.imp[d]);
-                    res = fmaxf(res, x * x);
-                }
-        } else {
-#pragma unroll
-            for (int d = 8; d >= 0; d--)
-                if (mt.imp[d] != 0.0f) {
-                    x = joint_row(d, 1.0f, mot_rhs[d], mot_lam[d], -mt.imp[d], mt.imp[d]);
-                    res = fmaxf(res, x * x);
-                }
-#pragma unroll
-            for (int d = 8; d >= 0; d--)
-#pragma unroll
-                for (int side = 1; side >= 0; side--)
-                    if (lim_on[d][side]) {
-                        x = joint_row(d, side ? -1.0f : 1.0f, lim_rhs[d][side], lim_lam[d][side], 0.0f,
-                                      (float)PM_LIMIT_MAX_IMPULSE);
-                        res = fmaxf(res, x * x);
-                    }
-        }
+    auto contacts = [&]() {
         // normals: ground contacts then gripper contacts
         if constexpr (HAS_CUBE) {
 #pragma unroll
             for (int c = 0; c < NG; c++)
-                if (c < ng) {
+                if (__builtin_amdgcn_ballot_w64(c < ng)) {
                     GroundContact &g = gc[c];
                     V3 rn = mk(g.r.y, -g.r.x, 0.0f);  // r x (0,0,1)
-                    float dl = g.rhs[0] - g.dinv[0] * (dot(rn, S.dw) + S.dvl.z);
-                    float sum = g.lam[0] + dl;
-                    if (sum < 0.0f) { dl = -g.lam[0]; g.lam[0] = 0.0f; }
-                    else if (sum > (float)PM_CONTACT_UPPER) { dl = (float)PM_CONTACT_UPPER - g.lam[0]; g.lam[0] = (float)PM_CONTACT_UPPER; }
-                    else g.lam[0] = sum;
-                    S.dw = S.dw + rn * (dl * inv_I);
-                    S.dvl.z += dl * inv_m;
-                    x = g.dinv[0] != 0.0f ? dl / g.dinv[0] : 0.0f;
+                    float dl = g.rhs[0] - g.dinv[0] * (dot(rn, dw) + dvl.z);
+                    float nl = fminf(fmaxf(g.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
+                    dl = nl - g.lam[0];
+                    g.lam[0] = nl;
+                    dw = dw + rn * (dl * inv_I);
+                    dvl.z += dl * inv_m;
+                    float x = dl * res_scale(g.dinv[0]);
                     res = fmaxf(res, x * x);
                 }
         }
 #pragma unroll
         for (int c = 0; c < NR; c++)
-            if (c < nr) {
+            if (__builtin_amdgcn_ballot_w64(c < nr)) {
                 RobotContact &r = rc[c];
-                float jv = jrow_dot(r.J[0], S.dv);
-                V3 rn;
-                if (HAS_CUBE && r.on_cube) {
-                    rn = cross(r.rB, r.dir[0]);
-                    jv -= dot(rn, S.dw) + dot(r.dir[0], S.dvl);
-                }
+                float jv = jrow_dot(r.J[0], dv);
+                if (HAS_CUBE) jv -= dot(r.rn[0], dw) + dot(r.dir[0], dvl);
                 float dl = r.rhs[0] - r.dinv[0] * jv;
-                float sum = r.lam[0] + dl;
-                if (sum < 0.0f) { dl = -r.lam[0]; r.lam[0] = 0.0f; }
-                else if (sum > (float)PM_CONTACT_UPPER) { dl = (float)PM_CONTACT_UPPER - r.lam[0]; r.lam[0] = (float)PM_CONTACT_UPPER; }
-                else r.lam[0] = sum;
+                float nl = fminf(fmaxf(r.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
+                dl = nl - r.lam[0];
+                r.lam[0] = nl;
 #pragma unroll
-                for (int a = 0; a < 9; a++) S.dv[a] += r.MJ[0][a] * dl;
-                if (HAS_CUBE && r.on_cube) {
-                    S.dw = S.dw - rn * (dl * inv_I);
-                    S.dvl = S.dvl - r.dir[0] * (dl * inv_m);
+                for (int a = 0; a < 9; a++) dv[a] += L.at(c, 0, a) * dl;
+                if (HAS_CUBE) {
+                    dw = dw - r.rn[0] * (dl * inv_I);
+                    dvl = dvl - r.dir[0] * (dl * inv_m);
                 }
-                x = r.dinv[0] != 0.0f ? dl / r.dinv[0] : 0.0f;
+                float x = dl * res_scale(r.dinv[0]);
                 res = fmaxf(res, x * x);
             }
         // friction cones
         if constexpr (HAS_CUBE) {
 #pragma unroll
             for (int c = 0; c < NG; c++)
-                if (c < ng) {
+                if (__builtin_amdgcn_ballot_w64(c < ng)) {
                     GroundContact &g = gc[c];
                     V3 r1 = mk(g.r.z, 0.0f, -g.r.x);  // r x (0,-1,0)
                     V3 r2 = mk(0.0f, g.r.z, -g.r.y);  // r x (1,0,0)
-                    float dla = g.rhs[1] - g.dinv[1] * (dot(r1, S.dw) - S.dvl.y);
-                    float dlb = g.rhs[2] - g.dinv[2] * (dot(r2, S.dw) + S.dvl.x);
+                    float dla = g.rhs[1] - g.dinv[1] * (dot(r1, dw) - dvl.y);
+                    float dlb = g.rhs[2] - g.dinv[2] * (dot(r2, dw) + dvl.x);
                     float sa = g.lam[1] + dla, sb = g.lam[2] + dlb;
                     float lim = (float)(PM_DEFAULT_FRICTION * PM_DEFAULT_FRICTION) * fmaxf(g.lam[0], 0.0f);
-                    float mag = sqrtf(sa * sa + sb * sb);
-                    if (mag > lim) {
-                        float s = mag > 0.0f ? lim / mag : 0.0f;
-                        sa *= s;
-                        sb *= s;
-                    }
+                    float m2 = sa * sa + sb * sb;
+                    // |f| > mu N: project onto the cone (lim * rsq(m2) <= 1 there)
+                    float s = m2 > lim * lim ? lim * rsqrtf(m2) : 1.0f;
+                    sa *= s;
+                    sb *= s;
                     dla = sa - g.lam[1];
                     dlb = sb - g.lam[2];
                     g.lam[1] = sa;
                     g.lam[2] = sb;
-                    S.dw = S.dw + (r1 * dla + r2 * dlb) * inv_I;
-                    S.dvl = S.dvl + mk(dlb, -dla, 0.0f) * inv_m;
-                    float ra = g.dinv[1] != 0.0f ? dla / g.dinv[1] : 0.0f;
-                    float rb = g.dinv[2] != 0.0f ? dlb / g.dinv[2] : 0.0f;
-                    x = fabsf(ra) > fabsf(rb) ? ra : rb;
+                    dw = dw + (r1 * dla + r2 * dlb) * inv_I;
+                    dvl = dvl + mk(dlb, -dla, 0.0f) * inv_m;
+                    float ra = dla * res_scale(g.dinv[1]), rb = dlb * res_scale(g.dinv[2]);
+                    float x = fabsf(ra) > fabsf(rb) ? ra : rb;
                     res = fmaxf(res, x * x);
                 }
         }
 #pragma unroll
         for (int c = 0; c < NR; c++)
-            if (c < nr) {
+            if (__builtin_amdgcn_ballot_w64(c < nr)) {
                 RobotContact &r = rc[c];
-                float ja = jrow_dot(r.J[1], S.dv), jb = jrow_dot(r.J[2], S.dv);
-                V3 r1, r2;
-                if (HAS_CUBE && r.on_cube) {
-                    r1 = cross(r.rB, r.dir[1]);
-                    r2 = cross(r.rB, r.dir[2]);
-                    ja -= dot(r1, S.dw) + dot(r.dir[1], S.dvl);
-                    jb -= dot(r2, S.dw) + dot(r.dir[2], S.dvl);
+                float ja = jrow_dot(r.J[1], dv), jb = jrow_dot(r.J[2], dv);
+                if (HAS_CUBE) {
+                    ja -= dot(r.rn[1], dw) + dot(r.dir[1], dvl);
+                    jb -= dot(r.rn[2], dw) + dot(r.dir[2], dvl);
                 }
                 float dla = r.rhs[1] - r.dinv[1] * ja, dlb = r.rhs[2] - r.dinv[2] * jb;
                 float sa = r.lam[1] + dla, sb = r.lam[2] + dlb;
                 float lim = r.mu * fmaxf(r.lam[0], 0.0f);
-                float mag = sqrtf(sa * sa + sb * sb);
-                if (mag > lim) {
-                    float s = mag > 0.0f ? lim / mag : 0.0f;
-                    sa *= s;
-                    sb *= s;
-                }
+                float m2 = sa * sa + sb * sb;
+                float s = m2 > lim * lim ? lim * rsqrtf(m2) : 1.0f;
+                sa *= s;
+                sb *= s;
                 dla = sa - r.lam[1];
                 dlb = sb - r.lam[2];
                 r.lam[1] = sa;
                 r.lam[2] = sb;
 #pragma unroll
-                for (int a = 0; a < 9; a++) S.dv[a] += r.MJ[1][a] * dla + r.MJ[2][a] * dlb;
-                if (HAS_CUBE && r.on_cube) {
-                    S.dw = S.dw - (r1 * dla + r2 * dlb) * inv_I;
-                    S.dvl = S.dvl - (r.dir[1] * dla + r.dir[2] * dlb) * inv_m;
+                for (int a = 0; a < 9; a++) dv[a] += L.at(c, 1, a) * dla + L.at(c, 2, a) * dlb;
+                if (HAS_CUBE) {
+                    dw = dw - (r.rn[1] * dla + r.rn[2] * dlb) * inv_I;
+                    dvl = dvl - (r.dir[1] * dla + r.dir[2] * dlb) * inv_m;
                 }
-                float ra = r.dinv[1] != 0.0f ? dla / r.dinv[1] : 0.0f;
-                float rb = r.dinv[2] != 0.0f ? dlb / r.dinv[2] : 0.0f;
-                x = fabsf(ra) > fabsf(rb) ? ra : rb;
+                float ra = dla * res_scale(r.dinv[1]), rb = dlb * res_scale(r.dinv[2]);
+                float x = fabsf(ra) > fabsf(rb) ? ra : rb;
                 res = fmaxf(res, x * x);
             }
+    };
+
+    // btSequentialImpulseConstraintSolver alternates the order of the
+    // non-contact rows by iteration parity: even iterations run them in
+    // reverse (motors 8..0, then limits 8..0), odd ones forward (limits 0..8,
+    // then motors 0..8).  The loop is unrolled by two so both orders are
+    // straight-line code; each env still stops at its own residual.
+    static_assert(PM_SOLVER_ITERATIONS % 2 == 0, "iteration pairs");
+    for (int it = 0; it < PM_SOLVER_ITERATIONS; it += 2) {
+        L = lds.opaque();
+        res = 0.0f;
+#pragma unroll
+        for (int d = 8; d >= 0; d--) motor_row(d);
+        if (__builtin_amdgcn_ballot_w64(lim_on != 0u)) {
+#pragma unroll
+            for (int d = 8; d >= 0; d--) limit_row(d);
+        }
+        contacts();
+        if (res <= (float)PM_SOLVER_RESIDUAL_THRESHOLD) break;
+        L = lds.opaque();
+        res = 0.0f;
+        if (__builtin_amdgcn_ballot_w64(lim_on != 0u)) {
+#pragma unroll
+            for (int d = 0; d < 9; d++) limit_row(d);
+        }
+#pragma unroll
+        for (int d = 0; d < 9; d++) motor_row(d);
+        contacts();
         if (res <= (float)PM_SOLVER_RESIDUAL_THRESHOLD) break;
     }
 
     // ---- integrate (btMultiBody::stepPositionsMultiDof)
 #pragma unroll
     for (int d = 0; d < 9; d++) {
-        qd[d] = v1[d] + S.dv[d];
+        qd[d] = v1[d] + dv[d];
         q[d] += dt * qd[d] + split_dq[d];
     }
     if constexpr (HAS_CUBE) {
-        cb.omg = cw1 + S.dw;
-        cb.vel = cv1 + S.dvl;
+        cb.omg = cw1 + dw;
+        cb.vel = cv1 + dvl;
         cb.pos = cb.pos + cb.vel * dt;
         float ang = norm(cb.omg);
         if (ang * dt > 0.5f * 1.5707963267948966f) ang = 0.5f * 1.5707963267948966f / dt;

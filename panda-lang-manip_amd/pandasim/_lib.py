@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpandasim.so")
+LIB_PATH = os.environ.get("PANDASIM_LIB", os.path.join(HERE, "libpandasim.so"))
 
 PS_OK = 0
 ERRORS = {-1: "PS_ERR_ARG", -2: "PS_ERR_HIP", -3: "PS_ERR_UNSUPPORTED"}
