@@ -76,8 +76,8 @@ def load_pmc_traffic(workload: str):
     if not os.path.exists(path):
         return None
     try:
-        data = json.load(open(path))
-        return data.get(workload)
+        entry = json.load(open(path)).get(workload)
+        return None if entry is None else entry["bytes_per_launch"]
     except Exception:
         return None
 

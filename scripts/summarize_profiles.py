@@ -1,0 +1,127 @@
+#!/usr/bin/env python
+"""Condense rocprofv3 output (gpurun_out/prof_*) into the committed summaries
+under profiles/:
+
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary
+  profiles/<tag>_summary.json       per-kernel durations (all launches and the
+                                    timed tail), resources, PMC bytes per launch
+  profiles/pmc_traffic.json         {workload: HBM bytes per k_step launch}
+                                    read by bench.py for roofline.traffic
+
+HBM bytes follow /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE and
+WRITE_SIZE (KiB) from separate --pmc passes; FETCH_SIZE is doubled on gfx950
+(it tallies 128-B read requests at 64 B), and the calibration pass of
+scripts/calib_fetch.hip (same 4-B-per-lane access width as the step kernel)
+reports the factor actually observed, which replaces the default 2.0 when
+present.
+
+usage: python scripts/summarize_profiles.py <tag> <workload> [--steps K]
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import json
+import os
+import shutil
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "gpurun_out")
+PROF = os.path.join(ROOT, "profiles")
+
+
+def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "")
+    return name.split("(")[0][:80]
+
+
+def counters(path, counter):
+    per = collections.defaultdict(list)
+    if not os.path.exists(path):
+        return per
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            per[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+    return per
+
+
+def calibrate():
+    """Observed bytes/counter ratios of scripts/calib_fetch.hip (4-B-per-lane
+    streams over 1 GiB) from gpurun_out/calib_{fetch,write}/ and calib.log."""
+    log = os.path.join(OUT, "calib.log")
+    if not os.path.exists(log):
+        return None
+    known = None
+    for line in open(log):
+        if line.startswith("{"):
+            known = json.loads(line)
+    if not known:
+        return None
+    f = counters(os.path.join(OUT, "calib_fetch", "run_counter_collection.csv"), "FETCH_SIZE").get("k_read")
+    w = counters(os.path.join(OUT, "calib_write", "run_counter_collection.csv"), "WRITE_SIZE").get("k_write")
+    out = dict(known)
+    if f:
+        out["fetch_kib_per_launch"] = sum(f) / len(f)
+        out["fetch_factor"] = known["read_bytes_per_launch"] / (out["fetch_kib_per_launch"] * 1024)
+    if w:
+        out["write_kib_per_launch"] = sum(w) / len(w)
+        out["write_factor"] = known["write_bytes_per_launch"] / (out["write_kib_per_launch"] * 1024)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag")
+    ap.add_argument("workload")
+    ap.add_argument("--steps", type=int, default=100, help="timed launches at the tail of the trace")
+    ap.add_argument("--kernel", default="k_step")
+    ap.add_argument("--prefix", default="prof")
+    args = ap.parse_args()
+    os.makedirs(PROF, exist_ok=True)
+    tdir = os.path.join(OUT, f"{args.prefix}_trace")
+    shutil.copy(os.path.join(tdir, "run_kernel_stats.csv"), os.path.join(PROF, f"{args.tag}_kernel_stats.csv"))
+
+    durs = collections.defaultdict(list)
+    res = {}
+    for r in csv.DictReader(open(os.path.join(tdir, "run_kernel_trace.csv"))):
+        k = short(r["Kernel_Name"])
+        durs[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        res[k] = {f: r[f] for f in ("LDS_Block_Size", "Scratch_Size", "VGPR_Count", "Accum_VGPR_Count", "SGPR_Count",
+                                    "Workgroup_Size_X", "Grid_Size_X")}
+    fetch = counters(os.path.join(OUT, f"{args.prefix}_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write = counters(os.path.join(OUT, f"{args.prefix}_write", "run_counter_collection.csv"), "WRITE_SIZE")
+
+    factor, calib = 2.0, calibrate()
+    if calib and calib.get("fetch_factor"):
+        factor = float(calib["fetch_factor"])
+
+    kernels = {}
+    for k, d in durs.items():
+        e = {"launches": len(d), "avg_ns_all": sum(d) / len(d), "resources": res[k]}
+        tail = d[-args.steps:]
+        e["avg_ns_tail"] = sum(tail) / len(tail)
+        if fetch.get(k):
+            e["fetch_kib_per_launch"] = sum(fetch[k]) / len(fetch[k])
+        if write.get(k):
+            e["write_kib_per_launch"] = sum(write[k]) / len(write[k])
+        if "fetch_kib_per_launch" in e and "write_kib_per_launch" in e:
+            e["hbm_bytes_per_launch"] = (e["fetch_kib_per_launch"] * factor + e["write_kib_per_launch"]) * 1024
+        kernels[k] = e
+    summary = {"tag": args.tag, "workload": args.workload, "fetch_factor": factor, "calibration": calib,
+               "kernels": kernels}
+    json.dump(summary, open(os.path.join(PROF, f"{args.tag}_summary.json"), "w"), indent=1)
+
+    step = [k for k in kernels if args.kernel in k]
+    if step and "hbm_bytes_per_launch" in kernels[step[0]]:
+        tpath = os.path.join(PROF, "pmc_traffic.json")
+        traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
+        traffic[args.workload] = {"bytes_per_launch": round(kernels[step[0]]["hbm_bytes_per_launch"]),
+                                  "source": f"profiles/{args.tag}_summary.json", "fetch_factor": factor}
+        json.dump(traffic, open(tpath, "w"), indent=1)
+    for k, e in sorted(kernels.items(), key=lambda kv: -kv[1]["avg_ns_all"] * kv[1]["launches"])[:4]:
+        print(k, {x: (round(v, 1) if isinstance(v, float) else v) for x, v in e.items() if x != "resources"})
+
+
+if __name__ == "__main__":
+    main()
