@@ -67,7 +67,7 @@ def cpu_baseline(task: str, seconds: float):
         steps += 1
     dt = time.perf_counter() - t0
     return {"value": round(n_env * steps / dt, 2), "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n_env} envs x {steps} steps of PandaPush-v3 in {dt:.1f} s on 1 host thread "
+            "sample": f"{n_env} envs x {steps} steps of {task} (ee, sparse) in {dt:.1f} s on 1 host thread "
                       f"(fp64 oracle; PyBullet not installed)"}
 
 
@@ -105,21 +105,25 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     import pandasim
+    from pandasim.dist import EpisodeStats, gather_to_rank0, max_over_ranks, shard_seeds
     from pandasim.envs import REGISTRY
 
     B = args.batch
     env = pandasim.make(args.env_id, num_envs=B, device=dev)
     spec = REGISTRY[args.env_id]
-    seeds = 12345 + rank * B
-    env.reset(seed=seeds)
+    # rank r owns global envs [r*B, (r+1)*B), env g seeded 12345 + g
+    env.reset(seed=shard_seeds(12345, world * B, world, rank).numpy().astype("uint64"))
     gen = torch.Generator(device=dev)
     gen.manual_seed(0xC0FFEE + rank)
     n_act = args.warmup + args.steps
     actions = torch.rand(n_act, B, env.action_dim, device=dev, generator=gen) * 2 - 1
-    returns = torch.zeros(B, device=dev)
+    stats = EpisodeStats(B, dev)
 
     for k in range(args.warmup):
-        env.step(actions[k], copy=False)
+        obs, r, te, tr, info = env.step(actions[k], copy=False)
+        stats.update(r, te, tr)  # also loads every kernel the timed loop uses
+    gather_to_rank0(stats.packed())
+    stats = EpisodeStats(B, dev)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -132,20 +136,16 @@ def main():
         starts[k].record()
         obs, r, te, tr, info = env.step(a, copy=False)
         stops[k].record()
-        returns.add_(r)
-    if world > 1:
-        gathered = [torch.empty_like(returns) for _ in range(world)] if rank == 0 else None
-        dist.gather(returns, gathered, dst=0)
+        stats.update(r, te, tr)
+    # the one collective of the path: episode statistics to rank 0 (RCCL over xGMI)
+    episode_stats = gather_to_rank0(stats.packed())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kernel_ms = sum(s.elapsed_time(e) for s, e in zip(starts, stops)) / args.steps
-    t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dev)
 
     total_env_steps = world * B * args.steps
     value = total_env_steps / elapsed
@@ -174,6 +174,12 @@ def main():
                      "bytes_per_env_step": bytes_env},
     }
     if rank == 0:
+        ep = episode_stats.double().cpu()
+        done = ep[2] > 0
+        out["episodes"] = {"envs_with_finished_episode": int(done.sum()),
+                           "mean_last_return": round(float(ep[0][done].mean()), 4) if done.any() else None,
+                           "last_success_rate": round(float(ep[1][done].mean()), 4) if done.any() else None,
+                           "gathered_envs": int(ep.shape[1])}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(spec["task"], args.cpu_seconds)
         print(json.dumps(out), flush=True)

@@ -123,6 +123,29 @@ int ps_link_state(ps_ctx *ctx, const void *state, int link, float *pos, float *q
 int ps_inverse_kinematics(ps_ctx *ctx, const void *state, int link, const float *pos, const float *orn,
                           float *q_out, void *stream);
 
+/* --- pieces of the unfused (Robot/Task plugin) path, pandasim/core.py --- */
+
+#define PS_MAX_UNIFORM 8
+
+/* gymnasium.utils.seeding.np_random(seed) (core.py:244) for every env with
+ * mask[i] != 0 (mask == NULL: all): env i's generator becomes
+ * Generator(PCG64(SeedSequence(seeds[i]))).  seeds: device [B] uint64. */
+int ps_rng_seed(ps_ctx *ctx, void *state, const uint8_t *mask, const uint64_t *seeds, void *stream);
+
+/* np_random.uniform(low, high) with n = len(low) <= PS_MAX_UNIFORM
+ * (reach.py:52, push.py:78,85, pick_and_place.py:75-76; random() is
+ * uniform(0, 1)): n consecutive draws from each masked env's stream into
+ * out [B, n] f64 (device).  low/high are HOST arrays of n doubles. */
+int ps_rng_uniform(ps_ctx *ctx, void *state, const uint8_t *mask, int n, const double *low, const double *high,
+                   double *out, void *stream);
+
+/* getBasePositionAndOrientation / getEulerFromQuaternion / getBaseVelocity of
+ * the object body (pybullet.py:284-349): pos, euler, lin_vel, ang_vel [B,3],
+ * quat [B,4] (x,y,z,w); any output may be NULL.  PS_ERR_UNSUPPORTED if the
+ * scene has no object. */
+int ps_base_state(ps_ctx *ctx, const void *state, float *pos, float *quat, float *euler, float *lin_vel,
+                  float *ang_vel, void *stream);
+
 /* Task.compute_reward / is_success (reach.py:56-65, push.py:89-98),
  * vectorised for HER (core.py:226): n goal pairs [n,3], each f64 when its
  * *_is_double flag is set, else f32.  As numpy does, the distance is computed

@@ -21,6 +21,19 @@ struct ps_ctx {
     char err[256];
 };
 
+#ifdef PS_PROFILE_PHASES
+__device__ unsigned long long ps_phase_cycles[PS_NUM_PHASES];
+extern "C" int ps_debug_phase_cycles(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ps_phase_cycles), sizeof(unsigned long long) * PS_NUM_PHASES) != hipSuccess)
+        return PS_ERR_HIP;
+    if (reset) {
+        unsigned long long z[PS_NUM_PHASES] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(ps_phase_cycles), z, sizeof z) != hipSuccess) return PS_ERR_HIP;
+    }
+    return PS_OK;
+}
+#endif
+
 namespace {
 
 constexpr int kBlock = 64;
@@ -104,7 +117,8 @@ PS_D void store_motors(const StateView &s, int64_t i, const Motors &m) {
 // occupying 45 registers through the solver.  The index goes through an empty
 // asm so the loads cannot be hoisted out of the substep loop.
 template <bool HAS_CUBE, bool STD_MOTORS>
-PS_D void run_substeps(const KParams &P, int64_t i, int n, float q[9], float qd[9], Cube &cb, const MJStore &lds) {
+PS_D void run_substeps(const KParams &P, int64_t i, int n, float q[9], float qd[9], Cube &cb,
+                       const MJStore &lds PS_PROF_PARAM) {
     for (int st = 0; st < n; st++) {
         int64_t ii = i;
         asm volatile("" : "+v"(ii));
@@ -115,7 +129,7 @@ PS_D void run_substeps(const KParams &P, int64_t i, int n, float q[9], float qd[
         } else {
             load_motors(P.s, ii, m);
         }
-        substep<HAS_CUBE, STD_MOTORS>(P.sc, q, qd, m, cb, lds);
+        substep<HAS_CUBE, STD_MOTORS>(P.sc, q, qd, m, cb, lds PS_PROF_ARG);
     }
 }
 PS_D void load_cube(const StateView &s, int64_t i, Cube &c) {
@@ -297,6 +311,11 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
     if (i >= P.n) return;
     const StateView &s = P.s;
     constexpr bool HAS_CUBE = TASK != PS_TASK_REACH;
+#ifdef PS_PROFILE_PHASES
+    PhaseTimer pt;
+    pt.last = __builtin_amdgcn_s_memtime();
+    for (int k = 0; k < PS_NUM_PHASES; k++) pt.acc[k] = 0;
+#endif
     float q[9], qd[9];
     load_robot(s, i, q, qd);
     Cube cb;
@@ -306,9 +325,10 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
         set_action<CONTROL>(P, actions + i * P.action_dim, q, m);
         store_motors(s, i, m);
     }
+    PS_PHASE(6);
     __shared__ float smem[LDS_FLOATS * kBlock];
     MJStore lds{(lds_float *)(smem + threadIdx.x), kBlock};
-    run_substeps<HAS_CUBE, true>(P, i, PM_SUBSTEPS, q, qd, cb, lds);
+    run_substeps<HAS_CUBE, true>(P, i, PM_SUBSTEPS, q, qd, cb, lds PS_PROF_ARG);
     double g[3] = {s.goal[i], s.goal[s.stride + i], s.goal[2 * s.stride + i]};
     // obs of the stepped state
     float a0, a1, a2;
@@ -340,6 +360,11 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
     store_robot(s, i, q, qd);
     if constexpr (HAS_CUBE) store_cube(s, i, cb);
     write_obs<TASK>(P, i, q, qd, cb, g, obs, ag, dg);
+#ifdef PS_PROFILE_PHASES
+    PS_PHASE(7);
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < PS_NUM_PHASES; k++) atomicAdd((unsigned long long *)&ps_phase_cycles[k], (unsigned long long)pt.acc[k]);
+#endif
 }
 
 template <bool HAS_CUBE>
@@ -353,7 +378,12 @@ __global__ __launch_bounds__(kBlock) void k_sim_step(KParams P, int n_substeps) 
     if constexpr (HAS_CUBE) load_cube(s, i, cb);
     __shared__ float smem[LDS_FLOATS * kBlock];
     MJStore lds{(lds_float *)(smem + threadIdx.x), kBlock};
-    run_substeps<HAS_CUBE, false>(P, i, n_substeps, q, qd, cb, lds);
+#ifdef PS_PROFILE_PHASES
+    PhaseTimer pt;
+    pt.last = __builtin_amdgcn_s_memtime();
+    for (int k = 0; k < PS_NUM_PHASES; k++) pt.acc[k] = 0;
+#endif
+    run_substeps<HAS_CUBE, false>(P, i, n_substeps, q, qd, cb, lds PS_PROF_ARG);
     store_robot(s, i, q, qd);
     if constexpr (HAS_CUBE) store_cube(s, i, cb);
 }
@@ -413,6 +443,43 @@ __global__ __launch_bounds__(kBlock) void k_ik(KParams P, const float *pos, cons
     float out[9];
     inverse_kinematics<LINK>(q, t, o, out);
     for (int d = 0; d < 9; d++) q_out[i * 9 + d] = out[d];
+}
+
+// gymnasium.utils.seeding.np_random(seed) per env (core.py:244): the env's
+// generator becomes Generator(PCG64(SeedSequence(seeds[i])))
+__global__ __launch_bounds__(kBlock) void k_rng_seed(KParams P, const uint8_t *mask, const uint64_t *seeds) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n || (mask && !mask[i])) return;
+    store_rng(P.s, i, pcg_seed(seeds[i]));
+}
+
+// Generator.uniform(low[n], high[n]) per env: n consecutive draws from the
+// env's own stream (push.py:75-80 draws a 3-vector in one call)
+struct UniformArgs {
+    int n;
+    double lo[PS_MAX_UNIFORM], hi[PS_MAX_UNIFORM];
+};
+__global__ __launch_bounds__(kBlock) void k_rng_uniform(KParams P, const uint8_t *mask, UniformArgs u, double *out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n || (mask && !mask[i])) return;
+    Pcg r = load_rng(P.s, i);
+    for (int k = 0; k < u.n; k++) out[i * u.n + k] = uniform(r, u.lo[k], u.hi[k]);
+    store_rng(P.s, i, r);
+}
+
+// getBasePositionAndOrientation + getEulerFromQuaternion + getBaseVelocity of
+// the object (pybullet.py:284-349)
+__global__ __launch_bounds__(kBlock) void k_base_state(KParams P, float *pos, float *quat, float *euler, float *vel,
+                                                       float *avel) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    Cube c;
+    load_cube(P.s, i, c);
+    if (pos) { pos[i * 3] = c.pos.x; pos[i * 3 + 1] = c.pos.y; pos[i * 3 + 2] = c.pos.z; }
+    if (quat) { quat[i * 4] = c.quat.x; quat[i * 4 + 1] = c.quat.y; quat[i * 4 + 2] = c.quat.z; quat[i * 4 + 3] = c.quat.w; }
+    if (euler) { V3 e = euler_from_quat(c.quat); euler[i * 3] = e.x; euler[i * 3 + 1] = e.y; euler[i * 3 + 2] = e.z; }
+    if (vel) { vel[i * 3] = c.vel.x; vel[i * 3 + 1] = c.vel.y; vel[i * 3 + 2] = c.vel.z; }
+    if (avel) { avel[i * 3] = c.omg.x; avel[i * 3 + 1] = c.omg.y; avel[i * 3 + 2] = c.omg.z; }
 }
 
 __global__ __launch_bounds__(256) void k_compute_reward(int reward_type, const void *ag, int ag_dbl, const void *dg,
@@ -613,6 +680,38 @@ int ps_inverse_kinematics(ps_ctx *c, const void *state, int link, const float *p
         PS_IK_CASE(6) PS_IK_CASE(7) PS_IK_CASE(8) PS_IK_CASE(9) PS_IK_CASE(10) PS_IK_CASE(11)
 #undef PS_IK_CASE
     }
+    return check_launch(c);
+}
+
+int ps_rng_seed(ps_ctx *c, void *state, const uint8_t *mask, const uint64_t *seeds, void *stream) {
+    if (!c || !state || !seeds) return fail(c, PS_ERR_ARG, "null argument");
+    KParams P = params_of(c, state);
+    hipLaunchKernelGGL(k_rng_seed, grid_of(P.n, kBlock), dim3(kBlock), 0, (hipStream_t)stream, P, mask, seeds);
+    return check_launch(c);
+}
+
+int ps_rng_uniform(ps_ctx *c, void *state, const uint8_t *mask, int n, const double *low, const double *high,
+                   double *out, void *stream) {
+    if (!c || !state || !out || !low || !high || n < 1 || n > PS_MAX_UNIFORM)
+        return fail(c, PS_ERR_ARG, "bad argument");
+    KParams P = params_of(c, state);
+    UniformArgs u;
+    u.n = n;
+    for (int k = 0; k < PS_MAX_UNIFORM; k++) {
+        u.lo[k] = k < n ? low[k] : 0.0;
+        u.hi[k] = k < n ? high[k] : 0.0;
+    }
+    hipLaunchKernelGGL(k_rng_uniform, grid_of(P.n, kBlock), dim3(kBlock), 0, (hipStream_t)stream, P, mask, u, out);
+    return check_launch(c);
+}
+
+int ps_base_state(ps_ctx *c, const void *state, float *pos, float *quat, float *euler, float *lin_vel,
+                  float *ang_vel, void *stream) {
+    if (!c || !state) return fail(c, PS_ERR_ARG, "null argument");
+    if (!c->cfg.has_cube) return fail(c, PS_ERR_UNSUPPORTED, "scene has no object");
+    KParams P = params_of(c, (void *)state);
+    hipLaunchKernelGGL(k_base_state, grid_of(P.n, kBlock), dim3(kBlock), 0, (hipStream_t)stream, P, pos, quat, euler,
+                       lin_vel, ang_vel);
     return check_launch(c);
 }
 

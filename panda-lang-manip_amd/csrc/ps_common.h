@@ -14,6 +14,28 @@
 #define PS_D __device__ __forceinline__
 #define PS_HD __host__ __device__ __forceinline__
 
+// Phase timing (diagnostic build only, -DPS_PROFILE_PHASES; scripts/phase_profile.py):
+// each wave accumulates s_memtime deltas per phase and lane 0 adds them to
+// ps_phase_cycles at the end of the kernel.  Compiled out of the product.
+#define PS_NUM_PHASES 8
+#ifdef PS_PROFILE_PHASES
+struct PhaseTimer {
+    uint64_t last, acc[PS_NUM_PHASES];
+};
+#define PS_PROF_PARAM , PhaseTimer &pt
+#define PS_PROF_ARG , pt
+#define PS_PHASE(k)                                        \
+    do {                                                   \
+        uint64_t ps_t_now = __builtin_amdgcn_s_memtime();  \
+        pt.acc[k] += ps_t_now - pt.last;                   \
+        pt.last = ps_t_now;                                \
+    } while (0)
+#else
+#define PS_PROF_PARAM
+#define PS_PROF_ARG
+#define PS_PHASE(k) do {} while (0)
+#endif
+
 namespace ps {
 
 // ------------------------------------------------------------------ vectors

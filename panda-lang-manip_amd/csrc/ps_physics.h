@@ -484,13 +484,14 @@ PS_D float res_scale(float dinv) { return __builtin_amdgcn_rcpf(dinv); }
 // on all nine joints with the fixed Panda gains and forces, panda.py:40-56), so
 // only the targets are per-env; otherwise every gain comes from `mt`.
 template <bool HAS_CUBE, bool STD_MOTORS>
-PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cube &cb, const MJStore &lds) {
+PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cube &cb, const MJStore &lds PS_PROF_PARAM) {
     const float dt = (float)PM_TIMESTEP;
     float Mi[45], hb[9];
     Geo geo;
     // phases are fenced so the scheduler does not interleave them (each one's
     // transient state is large; overlapping them is what spilled to scratch)
     bias_forces(q, qd, hb);
+    PS_PHASE(0);
     __builtin_amdgcn_sched_barrier(0);
     {
         Kin k;
@@ -507,8 +508,10 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
         });
         mass_matrix(k, Mi);
     }
+    PS_PHASE(1);
     __builtin_amdgcn_sched_barrier(0);
     spd_inverse(Mi);
+    PS_PHASE(2);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int k = 0; k < 45; k++) lds.mi(k) = Mi[k];
@@ -753,6 +756,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
             }
         }
     }
+    PS_PHASE(3);
     __builtin_amdgcn_sched_barrier(0);
 
     // ---- projected Gauss-Seidel
@@ -916,6 +920,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
         if (res <= (float)PM_SOLVER_RESIDUAL_THRESHOLD) break;
     }
 
+    PS_PHASE(4);
     // ---- integrate (btMultiBody::stepPositionsMultiDof)
 #pragma unroll
     for (int d = 0; d < 9; d++) {
@@ -934,6 +939,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
         float nn = rsqrtf(nq.x * nq.x + nq.y * nq.y + nq.z * nq.z + nq.w * nq.w);
         cb.quat = Q4{nq.x * nn, nq.y * nn, nq.z * nn, nq.w * nn};
     }
+    PS_PHASE(5);
 }
 
 }  // namespace ps

@@ -3,8 +3,14 @@
 Host layer over libpandasim.so (HIP, gfx950).  See DESIGN.md.
 """
 from ._lib import PandasimError, lib
+from .core import PyBulletRobot, RobotTaskEnv, Task, TimeLimit
 from .envs import REGISTRY, PandaVecEnv, make
+from .panda_tasks import PandaPickAndPlaceEnv, PandaPushEnv, PandaReachEnv
+from .robots import Panda
 from .sim import PandaSim
+from .tasks import PickAndPlace, Push, Reach
 
-__all__ = ["make", "PandaVecEnv", "PandaSim", "REGISTRY", "PandasimError", "lib"]
+__all__ = ["make", "PandaVecEnv", "PandaSim", "REGISTRY", "PandasimError", "lib", "PyBulletRobot", "Task",
+           "RobotTaskEnv", "TimeLimit", "Panda", "Reach", "Push", "PickAndPlace", "PandaReachEnv", "PandaPushEnv",
+           "PandaPickAndPlaceEnv"]
 __version__ = "0.1.0"

@@ -13,6 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PANDASIM_LIB", os.path.join(HERE, "libpandasim.so"))
 
 PS_OK = 0
+PS_MAX_UNIFORM = 8
 ERRORS = {-1: "PS_ERR_ARG", -2: "PS_ERR_HIP", -3: "PS_ERR_UNSUPPORTED"}
 
 # float row indices of the SoA state (include/pandasim.h)
@@ -47,7 +48,7 @@ def exported_symbols():
     return [
         "ps_abi_version", "ps_default_config", "ps_state_layout", "ps_create", "ps_destroy", "ps_last_error",
         "ps_obs_dim", "ps_action_dim", "ps_init_state", "ps_reset", "ps_step", "ps_sim_step", "ps_link_state",
-        "ps_inverse_kinematics", "ps_compute_reward",
+        "ps_inverse_kinematics", "ps_compute_reward", "ps_rng_seed", "ps_rng_uniform", "ps_base_state",
     ]
 
 
@@ -77,6 +78,9 @@ def lib():
     L.ps_link_state.argtypes = [V, V, I, V, V, V, V, V]
     L.ps_inverse_kinematics.argtypes = [V, V, I, V, V, V, V]
     L.ps_compute_reward.argtypes = [I, V, I, V, I, V, V, I64, V]
+    L.ps_rng_seed.argtypes = [V, V, V, V, V]
+    L.ps_rng_uniform.argtypes = [V, V, V, I, P(C.c_double), P(C.c_double), V, V]
+    L.ps_base_state.argtypes = [V, V, V, V, V, V, V, V]
     for name in exported_symbols():
         getattr(L, name).restype = getattr(L, name).restype if name in ("ps_destroy", "ps_last_error") else I
     _lib = L

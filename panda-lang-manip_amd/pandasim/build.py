@@ -14,25 +14,35 @@ DEPS = ["pandasim.hip", "ps_common.h", "ps_physics.h", "ps_task.h"]
 HEADERS = [os.path.join(ROOT, "include", h) for h in ("pandasim.h", "panda_model.h")]
 
 
-def needs_build() -> bool:
-    if not os.path.exists(OUT):
+# diagnostic variants (never loaded by the product unless PANDASIM_LIB names them)
+VARIANTS = {"": [], "prof": ["-DPS_PROFILE_PHASES"]}
+
+
+def out_path(variant: str = "") -> str:
+    return OUT if not variant else os.path.join(HERE, f"libpandasim_{variant}.so")
+
+
+def needs_build(variant: str = "") -> bool:
+    out = out_path(variant)
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(OUT)
+    t = os.path.getmtime(out)
     return any(os.path.getmtime(p) > t for p in [os.path.join(CSRC, d) for d in DEPS] + HEADERS)
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and not needs_build():
-        return OUT
+def build(force: bool = False, verbose: bool = True, variant: str = "", extra=()) -> str:
+    out = out_path(variant)
+    if not force and not extra and not needs_build(variant):
+        return out
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I", os.path.join(ROOT, "include"),
-           "-o", OUT + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
+           *VARIANTS[variant], *extra, "-o", out + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, variant="prof" if "--prof" in sys.argv else "")

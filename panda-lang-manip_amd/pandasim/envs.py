@@ -173,11 +173,22 @@ for _reward in ("sparse", "dense"):
                                  max_episode_steps=100 if _name == "Stack" else 50)
 
 
-def make(env_id: str, num_envs: int = 1, device="cuda", **kwargs) -> PandaVecEnv:
-    """gym.make(env_id) counterpart returning B envs."""
+def make(env_id: str, num_envs: int = 1, device="cuda", fused: bool = True, **kwargs):
+    """gym.make(env_id) counterpart returning B envs.
+
+    fused=True (default): PandaVecEnv, the whole step in one kernel (ps_step),
+    TimeLimit and auto-reset inside.  fused=False: the Robot/Task plugin
+    composition of panda_tasks.py (pandasim.panda_tasks) wrapped in
+    TimeLimit(max_episode_steps), as gym.make builds the reference env."""
     if env_id not in REGISTRY:
         raise KeyError(f"unknown env id {env_id}")
     spec = REGISTRY[env_id]
     if spec["task"] is None:
         raise NotImplementedError(f"{env_id}: Slide/Stack/Flip are the next rows of SURVEY.md §8(f)")
+    if not fused:
+        from .core import TimeLimit
+        from .panda_tasks import ENV_CLASSES
+
+        env = ENV_CLASSES[spec["task"]](num_envs, device, spec["reward_type"], spec["control_type"], **kwargs)
+        return TimeLimit(env, spec["max_episode_steps"])
     return PandaVecEnv(spec["task"], spec["reward_type"], spec["control_type"], num_envs, device, **kwargs)

@@ -8,8 +8,10 @@ field reads/writes are tensor views of the state buffer.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import itertools
+import math
 from typing import Dict, Optional, Sequence
 
 import torch
@@ -39,13 +41,24 @@ class PandaSim:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.num_envs = int(num_envs)
         self.n_substeps = int(n_substeps)
-        self.cfg = config if config is not None else L.default_config(TASKS[task], CONTROLS[control_type],
-                                                                      REWARDS[reward_type])
+        if config is not None:
+            self.cfg = config
+        elif task is None:
+            # empty world, built up by loadURDF/create_* as PyBullet() + Robot/Task constructors do
+            self.cfg = L.default_config(0, 0, 0)
+            self.cfg.has_table = self.cfg.has_plane = self.cfg.has_cube = 0
+            self.cfg.base[0] = 0.0
+        else:
+            self.cfg = L.default_config(TASKS[task], CONTROLS[control_type], REWARDS[reward_type])
         self._lib = L.lib()
-        ctx = C.c_void_p()
-        L.check(self._lib.ps_create(C.byref(self.cfg), self.num_envs, self.device.index, C.byref(ctx)),
-                what="ps_create")
-        self._ctx = ctx
+        self._ctx = None
+        self._create_ctx()
+        # body name -> kind ("robot", "object", "ghost"); the registered tasks' names
+        self._bodies: Dict[str, str] = {"panda": "robot"}
+        if self.cfg.has_cube:
+            self._bodies["object"] = "object"
+        self._ghost_pos: Dict[str, torch.Tensor] = {}
+        self._ghost_orn: Dict[str, torch.Tensor] = {}
         self.layout = L.layout(self.num_envs)
         self.state = torch.zeros(self.layout.total_bytes, dtype=torch.uint8, device=self.device)
         self._bind_views()
@@ -54,6 +67,17 @@ class PandaSim:
         self._call("ps_init_state", self._ctx, _ptr(self.state), self._stream())
 
     # ---------------------------------------------------------------- plumbing
+    def _create_ctx(self):
+        """(Re)create the context for the current scene config.  The state
+        buffer's layout depends only on num_envs, so the state survives."""
+        if self._ctx:
+            self._lib.ps_destroy(self._ctx)
+            self._ctx = None
+        ctx = C.c_void_p()
+        L.check(self._lib.ps_create(C.byref(self.cfg), self.num_envs, self.device.index, C.byref(ctx)),
+                what="ps_create")
+        self._ctx = ctx
+
     def _bind_views(self):
         lay, s = self.layout, self.state
         n = lay.stride
@@ -104,6 +128,119 @@ class PandaSim:
             self.close()
         except Exception:
             pass
+
+    # ------------------------------------------------- scene construction
+    # pybullet.py:507-799.  The scene is compiled into the kernels
+    # (include/panda_model.h): these calls accept exactly the bodies of the
+    # Reach/Push/PickAndPlace scenes and raise NotImplementedError otherwise.
+    @contextlib.contextmanager
+    def no_rendering(self):
+        """pybullet.py:502-507 (rendering is not part of this path)."""
+        yield
+
+    def place_visualizer(self, target_position=None, distance=None, yaw=None, pitch=None) -> None:
+        """pybullet.py:499-508: camera placement; no-op without rendering."""
+
+    def loadURDF(self, body_name: str, fileName: str, basePosition=None, useFixedBase: bool = False,
+                 **kwargs) -> None:
+        """pybullet.py:522-529: only the fixed-base Franka Panda is modelled."""
+        if not str(fileName).endswith("franka_panda/panda.urdf") or not useFixedBase:
+            raise NotImplementedError(f"loadURDF({fileName!r}, useFixedBase={useFixedBase}): only the fixed-base "
+                                      "franka_panda/panda.urdf is compiled in")
+        base = [0.0, 0.0, 0.0] if basePosition is None else [float(x) for x in basePosition]
+        for k in range(3):
+            self.cfg.base[k] = base[k]
+        self._bodies = {n: k for n, k in self._bodies.items() if k != "robot"}
+        self._bodies[body_name] = "robot"
+        self._create_ctx()
+
+    def create_plane(self, z_offset: float) -> None:
+        """pybullet.py:726-739."""
+        if abs(z_offset - PLANE_Z) > 1e-12:
+            raise NotImplementedError(f"create_plane(z_offset={z_offset}): only z_offset={PLANE_Z} is compiled in")
+        self.cfg.has_plane = 1
+        self._create_ctx()
+
+    def create_table(self, length: float, width: float, height: float, x_offset: float = 0.0,
+                     lateral_friction=None, spinning_friction=None) -> None:
+        """pybullet.py:741-771."""
+        if (length, width, height, x_offset) != TABLE or lateral_friction is not None or spinning_friction is not None:
+            raise NotImplementedError(f"create_table{(length, width, height, x_offset)}: only {TABLE} is compiled in")
+        self.cfg.has_table = 1
+        self._create_ctx()
+
+    def create_box(self, body_name: str, half_extents, mass: float, position, rgba_color=None, specular_color=None,
+                   ghost: bool = False, lateral_friction=None, spinning_friction=None, texture=None) -> None:
+        """pybullet.py:584-626: the one dynamic cube of Push/PickAndPlace, or a ghost marker."""
+        if ghost:
+            self._add_ghost(body_name, position)
+            return
+        he = [float(x) for x in half_extents]
+        if self.cfg.has_cube or max(he) != min(he) or mass <= 0 or lateral_friction is not None \
+                or spinning_friction is not None:
+            raise NotImplementedError("create_box: one dynamic cube (equal half extents, default friction) is "
+                                      "compiled in")
+        self.cfg.has_cube = 1
+        self.cfg.cube_half = he[0]
+        self.cfg.cube_mass = float(mass)
+        if self.cfg.task == 0:
+            self.cfg.task = 1
+        self._bodies[body_name] = "object"
+        self._create_ctx()
+        self.set_base_pose(body_name, position, [0.0, 0.0, 0.0, 1.0])
+
+    def create_sphere(self, body_name: str, radius: float, mass: float, position, rgba_color=None,
+                      specular_color=None, ghost: bool = False) -> None:
+        """pybullet.py:665-693: ghost target markers only."""
+        if not ghost:
+            raise NotImplementedError("create_sphere: only ghost spheres (targets) are supported")
+        self._add_ghost(body_name, position)
+
+    def create_cylinder(self, *args, **kwargs) -> None:
+        """pybullet.py:628-663 (Slide): SURVEY.md §8(f), not built yet."""
+        raise NotImplementedError("create_cylinder: PandaSlide is a next row of SURVEY.md §8(f)")
+
+    def set_lateral_friction(self, body: str, link: int, lateral_friction: float) -> None:
+        """pybullet.py:773-785: the compiled-in gripper proxies carry panda.py:47-48's values."""
+        if not (self._bodies.get(body) == "robot" and int(link) in (9, 10) and lateral_friction == 1.0):
+            raise NotImplementedError("set_lateral_friction: only the Panda fingers' 1.0 is compiled in")
+
+    def set_spinning_friction(self, body: str, link: int, spinning_friction: float) -> None:
+        """pybullet.py:787-799."""
+        if not (self._bodies.get(body) == "robot" and int(link) in (9, 10) and spinning_friction == 0.001):
+            raise NotImplementedError("set_spinning_friction: only the Panda fingers' 0.001 is compiled in")
+
+    def _add_ghost(self, body_name: str, position) -> None:
+        self._bodies[body_name] = "ghost"
+        self._ghost_pos[body_name] = torch.zeros(self.num_envs, 3, dtype=torch.float64, device=self.device)
+        self._ghost_orn[body_name] = torch.zeros(self.num_envs, 4, dtype=torch.float64, device=self.device)
+        self._ghost_orn[body_name][:, 3] = 1.0
+        self.set_base_pose(body_name, position, [0.0, 0.0, 0.0, 1.0])
+
+    def _kind(self, body: str) -> str:
+        if body not in self._bodies:
+            raise KeyError(f"unknown body {body!r}")
+        return self._bodies[body]
+
+    # ------------------------------------------------------- per-env RNGs
+    def seed(self, seeds, mask=None) -> None:
+        """seeding.np_random(seed) per env (core.py:244): seeds [B] uint64 (int64 bits)."""
+        seeds = torch.as_tensor(seeds, device=self.device).to(torch.int64).reshape(self.num_envs).contiguous()
+        m = None if mask is None else torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        self._call("ps_rng_seed", self._ctx, _ptr(self.state), _ptr(m), _ptr(seeds), self._stream())
+
+    def uniform(self, low, high, mask=None) -> torch.Tensor:
+        """Generator.uniform(low, high) of every env's own PCG64 stream -> [B, n] float64."""
+        lo = [float(x) for x in (low if hasattr(low, "__len__") else [low])]
+        hi = [float(x) for x in (high if hasattr(high, "__len__") else [high])]
+        n = len(lo)
+        if n != len(hi) or not 1 <= n <= L.PS_MAX_UNIFORM:
+            raise ValueError("uniform: low/high must have the same length, 1..8")
+        out = torch.empty(self.num_envs, n, dtype=torch.float64, device=self.device)
+        m = None if mask is None else torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        self._call("ps_rng_uniform", self._ctx, _ptr(self.state), _ptr(m), n, (C.c_double * n)(*lo),
+                   (C.c_double * n)(*hi), _ptr(out), self._stream())
+        return out
 
     # ------------------------------------------------------------ stepping
     def step(self) -> None:
@@ -156,16 +293,52 @@ class PandaSim:
     def get_joint_velocity(self, body: str, joint: int) -> torch.Tensor:
         return self.f[L.F_QD + JOINT_TO_DOF[joint], :self.num_envs].clone()
 
+    def _base_state(self):
+        B = self.num_envs
+        pos, euler, vel, avel = (torch.empty(B, 3, device=self.device) for _ in range(4))
+        quat = torch.empty(B, 4, device=self.device)
+        self._call("ps_base_state", self._ctx, _ptr(self.state), _ptr(pos), _ptr(quat), _ptr(euler), _ptr(vel),
+                   _ptr(avel), self._stream())
+        return pos, quat, euler, vel, avel
+
     def get_base_position(self, body: str) -> torch.Tensor:
+        """getBasePositionAndOrientation[0] (pybullet.py:284-294)."""
+        kind = self._kind(body)
+        if kind == "ghost":
+            return self._ghost_pos[body].clone()
+        if kind == "robot":
+            return torch.tensor([float(x) for x in self.cfg.base], device=self.device).expand(self.num_envs, 3)
         return self.rows(L.F_CPOS, 3).clone()
 
     def get_base_orientation(self, body: str) -> torch.Tensor:
+        """getBasePositionAndOrientation[1] (pybullet.py:296-306), (x, y, z, w)."""
+        kind = self._kind(body)
+        if kind == "ghost":
+            return self._ghost_orn[body].clone()
+        if kind == "robot":
+            return torch.tensor([0.0, 0.0, 0.0, 1.0], device=self.device).expand(self.num_envs, 4)
         return self.rows(L.F_CQUAT, 4).clone()
 
+    def get_base_rotation(self, body: str, type: str = "euler") -> torch.Tensor:
+        """pybullet.py:308-325: getEulerFromQuaternion of the base orientation."""
+        if type == "quaternion":
+            return self.get_base_orientation(body)
+        if type != "euler":
+            raise ValueError("""type must be "euler" or "quaternion".""")
+        if self._kind(body) == "object":
+            return self._base_state()[2]
+        return euler_from_quaternion(self.get_base_orientation(body))
+
     def get_base_velocity(self, body: str) -> torch.Tensor:
+        """getBaseVelocity[0] (pybullet.py:327-337)."""
+        if self._kind(body) != "object":
+            return torch.zeros(self.num_envs, 3, device=self.device)
         return self.rows(L.F_CVEL, 3).clone()
 
     def get_base_angular_velocity(self, body: str) -> torch.Tensor:
+        """getBaseVelocity[1] (pybullet.py:339-349)."""
+        if self._kind(body) != "object":
+            return torch.zeros(self.num_envs, 3, device=self.device)
         return self.rows(L.F_COMG, 3).clone()
 
     # -------------------------------------------------------------- setters
@@ -182,9 +355,21 @@ class PandaSim:
                               if torch.as_tensor(angle).dim() else [angle])
 
     def set_base_pose(self, body: str, position, orientation) -> None:
-        """resetBasePositionAndOrientation (pybullet.py:427-439); velocity kept."""
-        self.set_rows(L.F_CPOS, position)
-        self.set_rows(L.F_CQUAT, orientation)
+        """resetBasePositionAndOrientation (pybullet.py:427-439); velocity kept.
+        A 3-vector orientation is Euler angles (getQuaternionFromEuler)."""
+        orientation = torch.as_tensor(orientation, dtype=torch.float64, device=self.device)
+        if orientation.shape[-1] == 3:
+            orientation = quaternion_from_euler(orientation)
+        kind = self._kind(body)
+        if kind == "robot":
+            raise NotImplementedError("the Panda base is fixed (loadURDF useFixedBase=True)")
+        if kind == "ghost":
+            pos = torch.as_tensor(position, dtype=torch.float64, device=self.device)
+            self._ghost_pos[body][:] = pos.expand(self.num_envs, 3)
+            self._ghost_orn[body][:] = orientation.expand(self.num_envs, 4)
+            return
+        self.set_rows(L.F_CPOS, torch.as_tensor(position, device=self.device).to(torch.float32))
+        self.set_rows(L.F_CQUAT, orientation.to(torch.float32))
 
     def control_joints(self, body: str, joints: Sequence[int], target_angles, forces) -> None:
         """setJointMotorControlArray(POSITION_CONTROL) (pybullet.py:462-477)."""
@@ -206,3 +391,32 @@ class PandaSim:
         self._call("ps_inverse_kinematics", self._ctx, _ptr(self.state), int(link), _ptr(pos), _ptr(orn), _ptr(out),
                    self._stream())
         return out
+
+
+# ---------------------------------------------------------------- helpers
+PLANE_Z = -0.4                      # tasks/*.py: create_plane(z_offset=-0.4)
+TABLE = (1.1, 0.7, 0.4, -0.3)       # tasks/*.py: create_table(length, width, height, x_offset)
+
+
+def euler_from_quaternion(q: torch.Tensor) -> torch.Tensor:
+    """getEulerFromQuaternion (Bullet btQuaternion::getEulerZYX convention, as
+    ps_task.h::euler_from_quat) for (..., 4) (x, y, z, w) tensors."""
+    x, y, z, w = q.unbind(-1)
+    sarg = -2.0 * (x * z - w * y)
+    roll = torch.atan2(2.0 * (y * z + w * x), w * w - x * x - y * y + z * z)
+    pitch = torch.asin(sarg.clamp(-1.0, 1.0))
+    yaw = torch.atan2(2.0 * (x * y + w * z), w * w + x * x - y * y - z * z)
+    lo, hi = sarg <= -0.99999, sarg >= 0.99999
+    roll = torch.where(lo | hi, torch.zeros_like(roll), roll)
+    pitch = torch.where(lo, torch.full_like(pitch, -0.5 * math.pi), torch.where(hi, torch.full_like(pitch, 0.5 * math.pi),
+                                                                              pitch))
+    yaw = torch.where(lo, 2.0 * torch.atan2(x, -y), torch.where(hi, 2.0 * torch.atan2(-x, y), yaw))
+    return torch.stack([roll, pitch, yaw], -1)
+
+
+def quaternion_from_euler(e: torch.Tensor) -> torch.Tensor:
+    """getQuaternionFromEuler (roll about x, pitch about y, yaw about z) -> (x, y, z, w)."""
+    r, p, y = (e * 0.5).unbind(-1)
+    cr, sr, cp, sp, cy, sy = torch.cos(r), torch.sin(r), torch.cos(p), torch.sin(p), torch.cos(y), torch.sin(y)
+    return torch.stack([sr * cp * cy - cr * sp * sy, cr * sp * cy + sr * cp * sy, cr * cp * sy - sr * sp * cy,
+                        cr * cp * cy + sr * sp * sy], -1)

@@ -1,0 +1,49 @@
+#!/usr/bin/env python
+"""Per-phase cycle split of the fused step kernel (diagnostic build
+libpandasim_prof.so, -DPS_PROFILE_PHASES): runs B envs for a few steps and
+prints the share of wave-cycles in each phase of k_step."""
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "panda-lang-manip_amd"))
+os.environ["PANDASIM_LIB"] = os.path.join(ROOT, "panda-lang-manip_amd", "pandasim", "libpandasim_prof.so")
+
+import torch  # noqa: E402
+
+import pandasim  # noqa: E402
+from pandasim import _lib as L  # noqa: E402
+
+NAMES = ["bias_forces", "fk+mass_matrix", "spd_inverse", "rows+contacts", "pgs", "integrate", "set_action+ik",
+         "obs/reward/reset/store"]
+
+
+def main():
+    env_id = sys.argv[1] if len(sys.argv) > 1 else "PandaPush-v3"
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
+    steps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+    env = pandasim.make(env_id, num_envs=B)
+    env.reset(seed=12345)
+    lib = L.lib()
+    lib.ps_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int]
+    buf = (C.c_ulonglong * 8)()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0xC0FFEE)
+    for k in range(5):
+        env.step(torch.rand(B, env.action_dim, device="cuda", generator=g) * 2 - 1, copy=False)
+    torch.cuda.synchronize()
+    lib.ps_debug_phase_cycles(buf, 1)
+    for k in range(steps):
+        env.step(torch.rand(B, env.action_dim, device="cuda", generator=g) * 2 - 1, copy=False)
+    torch.cuda.synchronize()
+    assert lib.ps_debug_phase_cycles(buf, 0) == 0
+    tot = sum(buf)
+    waves = (B + 63) // 64
+    print(f"{env_id} B={B}: {tot / waves / steps:.0f} wave-cycles per env-step")
+    for n, v in zip(NAMES, buf):
+        print(f"  {n:24s} {v / tot * 100:6.2f} %   {v / waves / steps / 20:10.0f} cyc/substep-equiv")
+
+
+if __name__ == "__main__":
+    main()

@@ -92,6 +92,14 @@ def main():
     fetch = counters(os.path.join(OUT, f"{args.prefix}_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = counters(os.path.join(OUT, f"{args.prefix}_write", "run_counter_collection.csv"), "WRITE_SIZE")
 
+    extra = collections.defaultdict(dict)
+    vpath = os.path.join(OUT, f"{args.prefix}_valu", "run_counter_collection.csv")
+    if os.path.exists(vpath):
+        acc = collections.defaultdict(lambda: collections.defaultdict(list))
+        for r in csv.DictReader(open(vpath)):
+            acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, cs in acc.items():
+            extra[k] = {c: sum(v) / len(v) for c, v in cs.items()}
     factor, calib = 2.0, calibrate()
     if calib and calib.get("fetch_factor"):
         factor = float(calib["fetch_factor"])
@@ -105,6 +113,8 @@ def main():
             e["fetch_kib_per_launch"] = sum(fetch[k]) / len(fetch[k])
         if write.get(k):
             e["write_kib_per_launch"] = sum(write[k]) / len(write[k])
+        if extra.get(k):
+            e["sq_counters_per_launch"] = extra[k]
         if "fetch_kib_per_launch" in e and "write_kib_per_launch" in e:
             e["hbm_bytes_per_launch"] = (e["fetch_kib_per_launch"] * factor + e["write_kib_per_launch"]) * 1024
         kernels[k] = e
@@ -120,7 +130,8 @@ def main():
                                   "source": f"profiles/{args.tag}_summary.json", "fetch_factor": factor}
         json.dump(traffic, open(tpath, "w"), indent=1)
     for k, e in sorted(kernels.items(), key=lambda kv: -kv[1]["avg_ns_all"] * kv[1]["launches"])[:4]:
-        print(k, {x: (round(v, 1) if isinstance(v, float) else v) for x, v in e.items() if x != "resources"})
+        print(k, {x: (round(v, 1) if isinstance(v, float) else v) for x, v in e.items()
+                  if x not in ("resources", "sq_counters_per_launch")})
 
 
 if __name__ == "__main__":

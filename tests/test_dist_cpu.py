@@ -1,0 +1,108 @@
+"""N>1 path on the CPU (gloo, world size 2 and 3): the batch partition owns
+every env exactly once with the single-GPU seeds, and the only collective
+(episode statistics to rank 0) reassembles the global batch in env order.
+No kernel is launched: per-rank step outputs are synthetic tensors."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from pandasim.dist import EpisodeStats, gather_to_rank0, max_over_ranks, shard_range, shard_seeds
+
+
+def test_shard_range_partitions_the_batch():
+    for B in (7, 8, 65536, 524288, 1000003):
+        for W in (1, 2, 3, 4, 8):
+            if B < W:
+                continue
+            owned = []
+            for r in range(W):
+                s, n = shard_range(B, W, r)
+                owned.append((s, n))
+            assert owned[0][0] == 0
+            for (s0, n0), (s1, _) in zip(owned, owned[1:]):
+                assert s1 == s0 + n0
+            assert owned[-1][0] + owned[-1][1] == B
+            assert max(n for _, n in owned) - min(n for _, n in owned) <= 1
+    with pytest.raises(ValueError):
+        shard_range(2, 4, 0)
+    with pytest.raises(ValueError):
+        shard_range(8, 2, 2)
+
+
+def test_shard_seeds_match_single_gpu_run():
+    full = shard_seeds(12345, 524288, 1, 0)
+    parts = torch.cat([shard_seeds(12345, 524288, 8, r) for r in range(8)])
+    assert torch.equal(full, parts)
+    assert int(parts[65536]) == 12345 + 65536  # rank 1's first env (bench.py)
+
+
+def test_episode_stats_update():
+    st = EpisodeStats(3, "cpu")
+    z = torch.zeros(3, dtype=torch.uint8)
+    st.update(torch.tensor([-1.0, -1.0, 0.0]), z, z)
+    st.update(torch.tensor([-1.0, 0.0, 0.0]), torch.tensor([0, 1, 0], dtype=torch.uint8),
+              torch.tensor([1, 0, 0], dtype=torch.uint8))
+    p = st.packed()
+    assert p[0].tolist() == [-2.0, -1.0, 0.0]
+    assert p[1].tolist() == [0.0, 1.0, 0.0]
+    assert p[2].tolist() == [1.0, 1.0, 0.0]
+    assert st.running.tolist() == [0.0, 0.0, 0.0]
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, global_batch, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        start, n = shard_range(global_batch, world, rank)
+        seeds = shard_seeds(12345, global_batch, world, rank)
+        st = EpisodeStats(n, "cpu")
+        # synthetic per-env outputs that depend only on the global env id
+        gid = torch.arange(start, start + n)
+        for k in range(5):
+            r = -((gid + k) % 3 == 0).float()
+            te = ((gid + k) % 4 == 0).to(torch.uint8)
+            tr = torch.full((n,), int(k == 4), dtype=torch.uint8)
+            st.update(r, te, tr)
+        full = gather_to_rank0(st.packed())
+        full_seeds = gather_to_rank0(seeds.to(torch.float64))
+        t = max_over_ranks(float(rank + 1), "cpu")
+        if rank == 0:
+            q.put((full.tolist(), full_seeds.tolist(), t))
+        else:
+            assert full is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_gather_reassembles_global_batch(world):
+    B = 12 * world
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, B, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    full, seeds, t = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # the same statistics computed on one process over the whole batch
+    st = EpisodeStats(B, "cpu")
+    gid = torch.arange(B)
+    for k in range(5):
+        st.update(-((gid + k) % 3 == 0).float(), ((gid + k) % 4 == 0).to(torch.uint8),
+                  torch.full((B,), int(k == 4), dtype=torch.uint8))
+    assert torch.equal(torch.tensor(full), st.packed())
+    assert seeds == [12345.0 + g for g in range(B)]
+    assert t == float(world)

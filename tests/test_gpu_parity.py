@@ -75,14 +75,12 @@ def test_kat_inverse_kinematics(ps):  # pybullet_test.py:254-266
 
 
 def test_kat_box_free_fall(ps):  # pybullet_test.py:56-64 (robot parked far away: no contact)
-    from pandasim import _lib as L
     from pandasim.sim import PandaSim
 
-    cfg = L.default_config(1, 0, 0)
-    cfg.has_table = cfg.has_plane = 0
-    cfg.base[0] = 10.0
-    cfg.cube_half = 0.5
-    sim = PandaSim(config=cfg, num_envs=4)
+    sim = PandaSim(task=None, num_envs=4)
+    sim.loadURDF(body_name="panda", fileName="franka_panda/panda.urdf", basePosition=[10.0, 0.0, 0.0],
+                 useFixedBase=True)
+    sim.create_box(body_name="my_box", half_extents=[0.5, 0.5, 0.5], mass=1.0, position=[0.0, 0.0, 0.0])
     sim.step()
     assert np.allclose(sim.get_base_velocity("my_box").cpu().numpy(), [0.0, 0.0, -0.392], atol=1e-3)
     assert np.allclose(sim.get_base_orientation("my_box").cpu().numpy(), [0, 0, 0, 1], atol=1e-3)

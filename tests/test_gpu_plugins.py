@@ -1,0 +1,149 @@
+"""GPU tests of the Robot/Task plugin path (pandasim.core/robots/tasks, the
+batched panda_gym/envs/core.py split) through libpandasim.so:
+
+  * reset goldens: goals/objects drawn through Task.np_random are bit-exact
+    with the reference's task classes (tests/golden/task_layer.npz);
+  * the plugin composition steps like the fused kernel (ps_step) from the
+    same state, within the fused-vs-oracle tolerances of test_gpu_parity;
+  * reward / success / TimeLimit / save-restore semantics of core.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_parity import TOL, _groups
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ps():
+    import pandasim
+
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    return pandasim
+
+
+ENV_IDS = {"reach": "PandaReach", "push": "PandaPush", "pick_and_place": "PandaPickAndPlace"}
+
+
+@pytest.mark.parametrize("task", ["reach", "push", "pick_and_place"])
+def test_plugin_reset_goldens_bit_exact(ps, golden, task):
+    seeds = golden["seeds"]
+    env = ps.make(f"{ENV_IDS[task]}-v3", num_envs=len(seeds), fused=False)
+    for r in range(golden[f"{task}_goal"].shape[1]):
+        obs, info = env.reset(seed=seeds if r == 0 else None)
+        assert env.task.goal.dtype == torch.float64
+        assert np.array_equal(env.task.get_goal().cpu().numpy(), golden[f"{task}_goal"][:, r])
+        assert np.array_equal(obs["desired_goal"].cpu().numpy(), golden[f"{task}_goal"][:, r].astype(np.float32))
+        if task != "reach":
+            cpos = env.sim.get_base_position("object").cpu().numpy()
+            assert np.array_equal(cpos, golden[f"{task}_object"][:, r].astype(np.float32))
+            tpos = env.sim.get_base_position("target").cpu().numpy()
+            assert np.array_equal(tpos, golden[f"{task}_goal"][:, r])
+
+
+@pytest.mark.parametrize("task,control", [("reach", "ee"), ("reach", "joints"), ("push", "ee"),
+                                          ("pick_and_place", "ee"), ("pick_and_place", "joints")])
+def test_plugin_path_matches_fused_kernel(ps, task, control):
+    """Teacher-forced: from the fused env's state, one plugin-path step and one
+    fused step agree within the fused-vs-oracle tolerances."""
+    from pandasim.envs import PandaVecEnv
+
+    B = 128
+    fused = PandaVecEnv(task, "dense", control, B, "cuda", autoreset=False)
+    fused.reset(seed=777)
+    env = ps.make(f"{ENV_IDS[task]}{'Joints' if control == 'joints' else ''}Dense-v3", num_envs=B, fused=False)
+    env.reset(seed=777)
+    assert torch.equal(env.task.get_goal(), fused.sim.goal[:, :B].t())
+    rng = np.random.default_rng(17)
+    groups = _groups(fused.obs_dim)
+    worst = {k: 0.0 for k in groups}
+    for s in range(8):
+        env.sim.state.copy_(fused.sim.state)
+        a = torch.from_numpy(rng.uniform(-1, 1, size=(B, fused.action_dim)).astype(np.float32)).cuda()
+        o_f, r_f, te_f, _, _ = fused.step(a)
+        o_p, r_p, te_p, tr_p, info = env.step(a)
+        assert o_p["observation"].shape == o_f["observation"].shape
+        assert torch.equal(o_p["desired_goal"], o_f["desired_goal"])
+        for k, idx in groups.items():
+            worst[k] = max(worst[k], float((o_p["observation"][:, idx] - o_f["observation"][:, idx]).abs().max()))
+        # dense reward = -distance: agrees to the achieved-goal tolerance
+        assert float((r_p - r_f).abs().max()) <= 2 * TOL[task]["ee_pos" if task == "reach" else "obj_pos"]
+        assert int((te_p != te_f.bool()).sum()) <= 2
+        assert torch.equal(info["is_success"], te_p)
+        assert not tr_p.any()
+    print(task, control, {k: f"{v:.2e}" for k, v in worst.items()})
+    for k, v in worst.items():
+        assert v <= TOL[task][k], (k, v)
+
+
+def test_plugin_reward_success_and_her_shapes(ps, golden):
+    env = ps.make("PandaPush-v3", num_envs=8, fused=False)
+    ag = torch.from_numpy(golden["reward_ag"]).cuda()
+    dg = torch.from_numpy(golden["reward_dg"]).cuda()
+    r = env.compute_reward(ag, dg, {}).cpu().numpy()
+    assert np.array_equal(r.view(np.uint32), golden["reward_sparse"].view(np.uint32))
+    assert np.array_equal(env.task.is_success(ag, dg).cpu().numpy(), golden["success"])
+    her = env.compute_reward(torch.from_numpy(golden["her_ag"]).cuda(), torch.from_numpy(golden["her_dg"]).cuda(), {})
+    assert np.array_equal(her.cpu().numpy().view(np.uint32), golden["her_reward_sparse"].view(np.uint32))
+    dense = ps.make("PandaPushDense-v3", num_envs=8, fused=False)
+    r = dense.compute_reward(ag, dg, {}).cpu().numpy()
+    assert np.array_equal(r.view(np.uint32), golden["reward_dense"].view(np.uint32))
+
+
+def test_plugin_time_limit_and_state_snapshots(ps):
+    env = ps.make("PandaReach-v3", num_envs=16, fused=False)
+    env.reset(seed=3)
+    zeros = torch.zeros(16, 3, device="cuda")
+    for k in range(49):
+        _, _, _, tr, _ = env.step(zeros)
+        assert not tr.any()
+    _, _, _, tr, _ = env.step(zeros)
+    assert tr.all()
+    env.reset(seed=4)
+    sid = env.save_state()
+    a = torch.rand(16, 3, device="cuda") * 2 - 1
+    o1, *_ = env.step(a)
+    env.reset(seed=5)
+    env.restore_state(sid)
+    o2, *_ = env.step(a)
+    for k in o1:
+        assert torch.equal(o1[k], o2[k])
+    env.remove_state(sid)
+    with pytest.raises(Exception):
+        env.restore_state(sid)
+
+
+def test_plugin_goal_required_and_scene_validation(ps):
+    from pandasim.sim import PandaSim
+    from pandasim.tasks import Push
+
+    sim = PandaSim(task=None, num_envs=4)
+    task = Push(sim)
+    with pytest.raises(RuntimeError):
+        task.get_goal()  # core.py:185-186
+    with pytest.raises(NotImplementedError):
+        sim.create_table(length=2.0, width=0.7, height=0.4, x_offset=-0.3)
+    with pytest.raises(NotImplementedError):
+        sim.loadURDF("ur5", "ur5/ur5.urdf", useFixedBase=True)
+    with pytest.raises(ValueError):
+        sim.get_base_rotation("object", type="axis")
+    with pytest.raises(KeyError):
+        sim.get_base_position("nope")
+
+
+def test_device_sqrt_and_distance_match_numpy(ps):
+    """utils.distance on the GPU is bit-exact with np.linalg.norm (float64
+    mixed pairs and float32 pairs)."""
+    from pandasim.utils import distance
+
+    rng = np.random.default_rng(1)
+    a32 = rng.uniform(-1, 1, size=(1 << 16, 3)).astype(np.float32)
+    b64 = rng.uniform(-1, 1, size=(1 << 16, 3))
+    b32 = b64.astype(np.float32)
+    for b in (b64, b32):
+        got = distance(torch.from_numpy(a32).cuda(), torch.from_numpy(b).cuda()).cpu().numpy()
+        ref = np.linalg.norm(a32 - b, axis=-1)
+        assert got.dtype == ref.dtype
+        assert np.array_equal(got, ref)

@@ -1,0 +1,115 @@
+"""CPU tests of the host layer's task logic (pandasim.tasks / utils / core):
+draw order, goal arithmetic, distance, reward and success against the
+reference task goldens, with a recording stand-in for PandaSim whose per-env
+generators are numpy's own PCG64 (the device kernels are covered by the -m gpu
+tests)."""
+import numpy as np
+import pytest
+import torch
+
+from pandasim.core import TimeLimit, np_random
+from pandasim.tasks import PickAndPlace, Push, Reach
+from pandasim.utils import angle_distance, distance
+
+
+class FakeSim:
+    """Scene calls are recorded; uniform() draws from numpy Generators."""
+
+    def __init__(self, n):
+        self.num_envs, self.device = n, torch.device("cpu")
+        self.gens = [np.random.Generator(np.random.PCG64(np.random.SeedSequence(i))) for i in range(n)]
+        self.calls = []
+        self.poses = {}
+
+    def no_rendering(self):
+        import contextlib
+        return contextlib.nullcontext()
+
+    def __getattr__(self, name):
+        if name.startswith(("create_", "place_")):
+            return lambda *a, **k: self.calls.append(name)
+        raise AttributeError(name)
+
+    def seed(self, seeds):
+        self.gens = [np.random.Generator(np.random.PCG64(np.random.SeedSequence(int(s)))) for s in
+                     seeds.numpy().view(np.uint64)]
+
+    def uniform(self, low, high):
+        return torch.from_numpy(np.stack([g.uniform(low, high) for g in self.gens]))
+
+    def set_base_pose(self, body, position, orientation):
+        self.poses[body] = torch.as_tensor(position).clone()
+
+    def get_base_position(self, body):
+        return self.poses[body].to(torch.float32)
+
+
+@pytest.mark.parametrize("task", ["reach", "push", "pick_and_place"])
+def test_task_reset_draw_order_matches_goldens(golden, task):
+    seeds = golden["seeds"]
+    sim = FakeSim(len(seeds))
+    if task == "reach":
+        t = Reach(sim, get_ee_position=lambda: torch.zeros(len(seeds), 3))
+    else:
+        t = (Push if task == "push" else PickAndPlace)(sim)
+    assert "create_table" in sim.calls and "create_plane" in sim.calls
+    for r in range(golden[f"{task}_goal"].shape[1]):
+        if r == 0:
+            t.np_random, _ = np_random(sim, seeds)
+        t.reset()
+        assert np.array_equal(t.get_goal().numpy(), golden[f"{task}_goal"][:, r])
+        assert np.array_equal(sim.poses["target"].numpy(), golden[f"{task}_goal"][:, r])
+        if task != "reach":
+            assert np.array_equal(sim.poses["object"].numpy(), golden[f"{task}_object"][:, r])
+
+
+def test_distance_reward_success_goldens(golden):
+    ag, dg = torch.from_numpy(golden["reward_ag"]), torch.from_numpy(golden["reward_dg"])
+    assert np.array_equal(distance(ag, dg).numpy(), np.linalg.norm(golden["reward_ag"] - golden["reward_dg"], axis=-1))
+    for rt in ("sparse", "dense"):
+        t = Push(FakeSim(1), reward_type=rt)
+        r = t.compute_reward(ag, dg, {}).numpy()
+        assert r.dtype == np.float32
+        assert np.array_equal(r.view(np.uint32), golden[f"reward_{rt}"].view(np.uint32))
+        her = t.compute_reward(torch.from_numpy(golden["her_ag"]), torch.from_numpy(golden["her_dg"]), {}).numpy()
+        assert np.array_equal(her.view(np.uint32), golden[f"her_reward_{rt}"].view(np.uint32))
+    assert np.array_equal(Push(FakeSim(1)).is_success(ag, dg).numpy(), golden["success"])
+
+
+def test_float32_distance_is_correctly_rounded():
+    rng = np.random.default_rng(0)
+    a = rng.uniform(-1, 1, size=(4096, 3)).astype(np.float32)
+    b = rng.uniform(-1, 1, size=(4096, 3)).astype(np.float32)
+    got = distance(torch.from_numpy(a), torch.from_numpy(b)).numpy()
+    assert got.dtype == np.float32
+    assert np.array_equal(got, np.linalg.norm(a - b, axis=-1))
+
+
+def test_angle_distance():
+    a = np.array([[0.0, 0.0, 0.0, 1.0], [0.0, 0.0, 1.0, 0.0]])
+    b = np.array([[0.0, 0.0, 0.0, 1.0], [0.0, 0.0, 0.0, 1.0]])
+    assert np.allclose(angle_distance(torch.from_numpy(a), torch.from_numpy(b)).numpy(), [0.0, 1.0])
+
+
+def test_distance_shape_mismatch_asserts():  # utils.py:14
+    with pytest.raises(AssertionError):
+        distance(torch.zeros(2, 3), torch.zeros(3, 3))
+
+
+def test_time_limit_wrapper():
+    class Dummy:
+        num_envs, device = 3, torch.device("cpu")
+
+        def reset(self, **kw):
+            return {}, {}
+
+        def step(self, a):
+            z = torch.zeros(3, dtype=torch.bool)
+            return {}, torch.zeros(3), z, z, {}
+
+    env = TimeLimit(Dummy(), 2)
+    env.reset()
+    assert not env.step(None)[3].any()
+    assert env.step(None)[3].all()
+    env.reset()
+    assert not env.step(None)[3].any()
