@@ -35,7 +35,9 @@ def build(force: bool = False, verbose: bool = True, variant: str = "", extra=()
     if not force and not extra and not needs_build(variant):
         return out
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-I", os.path.join(ROOT, "include"),
+    # -fno-slp-vectorize: SLP packing into v_pk_fma_f32 pairs made the register
+    # allocator spill 590 VGPRs of the step kernel to scratch
+    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC", "-shared", "-I", os.path.join(ROOT, "include"),
            *VARIANTS[variant], *extra, "-o", out + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
     if verbose:
         print(" ".join(cmd), flush=True)

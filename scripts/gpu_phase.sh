@@ -1,9 +1,9 @@
-# GPU pass: GPU parity tests of the in-tree build, phase split, bench line
+# GPU pass: phase split of the fused step kernel (diagnostic build) + bench line
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -q -m gpu -s > gpurun_out/pytest_gpu.log 2>&1 && \
 timeout -k 10 300 python scripts/phase_profile.py PandaPush-v3 65536 20 > gpurun_out/phase.log 2>&1 && \
 timeout -k 10 300 python scripts/phase_profile.py PandaReach-v3 65536 20 >> gpurun_out/phase.log 2>&1 && \
+timeout -k 10 300 python scripts/phase_profile.py PandaPickAndPlace-v3 65536 20 >> gpurun_out/phase.log 2>&1 && \
 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench.log 2>&1
 echo "done rc=$?"
