@@ -513,8 +513,13 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
     spd_inverse(Mi);
     PS_PHASE(2);
     __builtin_amdgcn_sched_barrier(0);
+    // M^-1 for the joint rows: registers when the scene leaves room (no
+    // object: Reach), else LDS (re-read every PGS iteration)
+    constexpr bool MI_REGS = !HAS_CUBE;
+    if constexpr (!MI_REGS) {
 #pragma unroll
-    for (int k = 0; k < 45; k++) lds.mi(k) = Mi[k];
+        for (int k = 0; k < 45; k++) lds.mi(k) = Mi[k];
+    }
     float v1[9];
 #pragma unroll
     for (int a = 0; a < 9; a++) {
@@ -777,9 +782,14 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
         dl = nl - lam;
         lam = nl;
         float f = sgn * dl;
+        if constexpr (MI_REGS) {
 #pragma unroll
-        for (int a = 0; a < 9; a++) dv[a] += L.mi(sidx(a, d)) * f;
-        float x = dl * L.mi(sidx(d, d));  // residual dl / dinv = dl * (J M^-1 J^T)
+            for (int a = 0; a < 9; a++) dv[a] += Mi[sidx(a, d)] * f;
+        } else {
+#pragma unroll
+            for (int a = 0; a < 9; a++) dv[a] += L.mi(sidx(a, d)) * f;
+        }
+        float x = dl * (MI_REGS ? Mi[sidx(d, d)] : (float)L.mi(sidx(d, d)));  // residual dl / dinv
         res = fmaxf(res, x * x);
     };
     auto limit_row = [&](int d) {
