@@ -422,11 +422,20 @@ PS_D void plane_space(V3 n, V3 &p, V3 &q) {
 
 constexpr int NG = PM_MAX_GROUND_CONTACTS;
 constexpr int NR = PM_MAX_ROBOT_CONTACTS;
-// LDS floats per lane: M^-1 J^T of the 3 rows of every gripper contact, then
-// the packed M^-1 (read by the joint rows).  153 floats x 256 lanes per CU =
-// 153 KiB of the 160 KiB LDS at one wave per SIMD.
-constexpr int LDS_MI_OFFSET = NR * 27;
+// LDS floats per lane: M^-1 J^T of the 3 rows of every gripper contact
+// (108 floats x 256 lanes per CU = 108 KiB of the 160 KiB LDS at one wave per
+// SIMD); the diagnostic PS_MI_LDS build appends the packed M^-1.
+// Then 40 floats of per-substep values the PGS loop never reads (q, v1, the
+// split-impulse position correction, the object's pre-solve velocities and
+// pose): they wait in LDS across the solve instead of holding registers.
+constexpr int LDS_STASH_OFFSET = NR * 27;
+constexpr int LDS_STASH_FLOATS = 40;
+constexpr int LDS_MI_OFFSET = LDS_STASH_OFFSET + LDS_STASH_FLOATS;
+#ifdef PS_MI_LDS
 constexpr int LDS_FLOATS = LDS_MI_OFFSET + 45;
+#else
+constexpr int LDS_FLOATS = LDS_MI_OFFSET;
+#endif
 
 // cube-ground contact: cube-only rows; normal +z, friction dirs of planeSpace(+z) = (0,-1,0), (1,0,0)
 struct GroundContact {
@@ -449,6 +458,7 @@ struct MJStore {
     int stride;
     PS_D lds_float &at(int slot, int row, int k) const { return base[((slot * 3 + row) * 9 + k) * stride]; }
     PS_D lds_float &mi(int k) const { return base[(LDS_MI_OFFSET + k) * stride]; }
+    PS_D lds_float &stash(int k) const { return base[(LDS_STASH_OFFSET + k) * stride]; }
     // a copy whose address the compiler cannot see through: loads from it are
     // not loop-invariant, so they stay in the PGS loop as ds_reads instead of
     // being hoisted into (spilled) registers
@@ -513,9 +523,15 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
     spd_inverse(Mi);
     PS_PHASE(2);
     __builtin_amdgcn_sched_barrier(0);
-    // M^-1 for the joint rows: registers when the scene leaves room (no
-    // object: Reach), else LDS (re-read every PGS iteration)
-    constexpr bool MI_REGS = !HAS_CUBE;
+    // M^-1 for the joint rows stays in registers: re-reading it from LDS in
+    // every PGS iteration exposed the LDS latency once per motor row (Push
+    // 4.56 -> 3.99 ms, Reach 2.97 -> 1.98 ms per step of 65 536 envs).
+    // PS_MI_LDS keeps the LDS variant for comparison.
+#ifdef PS_MI_LDS
+    constexpr bool MI_REGS = false;
+#else
+    constexpr bool MI_REGS = true;
+#endif
     if constexpr (!MI_REGS) {
 #pragma unroll
         for (int k = 0; k < 45; k++) lds.mi(k) = Mi[k];
@@ -763,6 +779,18 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
     }
     PS_PHASE(3);
     __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int d = 0; d < 9; d++) {
+        lds.stash(d) = q[d];
+        lds.stash(9 + d) = v1[d];
+        lds.stash(18 + d) = split_dq[d];
+    }
+    if constexpr (HAS_CUBE) {
+        lds.stash(27) = cw1.x; lds.stash(28) = cw1.y; lds.stash(29) = cw1.z;
+        lds.stash(30) = cv1.x; lds.stash(31) = cv1.y; lds.stash(32) = cv1.z;
+        lds.stash(33) = cb.pos.x; lds.stash(34) = cb.pos.y; lds.stash(35) = cb.pos.z;
+        lds.stash(36) = cb.quat.x; lds.stash(37) = cb.quat.y; lds.stash(38) = cb.quat.z; lds.stash(39) = cb.quat.w;
+    }
 
     // ---- projected Gauss-Seidel
     // Every row kind is gated by a wave-uniform ballot (a scalar branch: the
@@ -931,6 +959,23 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
     }
 
     PS_PHASE(4);
+    {
+        // reload through an opaque address: no store-to-load forwarding, so
+        // the registers really were free during the solve
+        MJStore S = lds.opaque();
+#pragma unroll
+        for (int d = 0; d < 9; d++) {
+            q[d] = S.stash(d);
+            v1[d] = S.stash(9 + d);
+            split_dq[d] = S.stash(18 + d);
+        }
+        if constexpr (HAS_CUBE) {
+            cw1 = mk(S.stash(27), S.stash(28), S.stash(29));
+            cv1 = mk(S.stash(30), S.stash(31), S.stash(32));
+            cb.pos = mk(S.stash(33), S.stash(34), S.stash(35));
+            cb.quat = Q4{S.stash(36), S.stash(37), S.stash(38), S.stash(39)};
+        }
+    }
     // ---- integrate (btMultiBody::stepPositionsMultiDof)
 #pragma unroll
     for (int d = 0; d < 9; d++) {

@@ -1,0 +1,36 @@
+#!/usr/bin/env python
+"""Build experimental libpandasim variants (extra compiler flags) into
+scripts/bin/variants/ for scripts/time_variants.py."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "panda-lang-manip_amd"))
+from pandasim import build as B  # noqa: E402
+
+VARIANTS = {
+    "base": [],
+    "maxilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    "bias0": ["-mllvm", "-amdgpu-schedule-metric-bias=0"],
+    "mi_lds": ["-DPS_MI_LDS"],
+}
+
+
+def main(names):
+    out_dir = os.path.join(ROOT, "scripts", "bin", "variants")
+    os.makedirs(out_dir, exist_ok=True)
+    procs = []
+    for n in names:
+        out = os.path.join(out_dir, f"lib_{n}.so")
+        cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC",
+               "-shared", "-I", os.path.join(ROOT, "include"), *VARIANTS[n], "-o", out,
+               os.path.join(B.CSRC, "pandasim.hip")]
+        procs.append((n, subprocess.Popen(cmd, stderr=subprocess.PIPE, text=True)))
+    for n, p in procs:
+        _, err = p.communicate()
+        print(n, "ok" if p.returncode == 0 else err[-2000:])
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or list(VARIANTS))
