@@ -25,13 +25,14 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_TFLOPS = 157.3
 
 
-def algorithmic_bytes_per_env_step(obs_dim: int, action_dim: int) -> int:
+def algorithmic_bytes_per_env_step(obs_dim: int, action_dim: int, goal_dim: int = 3, n_objects: int = 1) -> int:
     """Bytes one env-step must move through HBM:
-    read q,qd (18 f32), object 13 f32, goal 3 f64, TimeLimit counter, action;
-    write q,qd, 45 motor f32, object, counter, obs, ag, dg, reward, 2 flags,
-    final_obs + final_ag."""
-    read = 18 * 4 + 13 * 4 + 3 * 8 + 4 + action_dim * 4
-    write = 18 * 4 + 45 * 4 + 13 * 4 + 4 + obs_dim * 4 + 12 + 12 + 4 + 2 + obs_dim * 4 + 12
+    read q,qd (18 f32), 13 f32 per object, goal (f64), TimeLimit counter,
+    action; write q,qd, 45 motor f32, objects, counter, obs, ag, dg (f32),
+    reward, 2 flags, final_obs + final_ag.  PandaPush-v3: 658 B."""
+    read = 18 * 4 + 13 * 4 * n_objects + goal_dim * 8 + 4 + action_dim * 4
+    write = (18 * 4 + 45 * 4 + 13 * 4 * n_objects + 4 + obs_dim * 4 + 2 * goal_dim * 4 + 4 + 2 + obs_dim * 4
+             + goal_dim * 4)
     return read + write
 
 
@@ -149,7 +150,7 @@ def main():
 
     total_env_steps = world * B * args.steps
     value = total_env_steps / elapsed
-    bytes_env = algorithmic_bytes_per_env_step(env.obs_dim, env.action_dim)
+    bytes_env = algorithmic_bytes_per_env_step(env.obs_dim, env.action_dim, env.goal_dim, env.sim.cfg.n_objects)
     achieved = bytes_env * B / (kernel_ms * 1e-3) / 1e9
     workload = f"{args.env_id} x{B}/gpu"
     out = {
@@ -170,7 +171,7 @@ def main():
                    "global_batch": world * B, "substeps": 20, "parallelism": f"batch shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": load_pmc_traffic(workload),
-                     "kernel": "k_step<PUSH,EE>", "kernel_ms": round(kernel_ms, 4),
+                     "kernel": f"k_step<{spec['task'].upper()},{spec['control_type'].upper()}>", "kernel_ms": round(kernel_ms, 4),
                      "bytes_per_env_step": bytes_env},
     }
     if rank == 0:

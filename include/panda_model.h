@@ -146,8 +146,36 @@
 #define PM_MAX_GROUND_CONTACTS 4
 #define PM_MAX_ROBOT_CONTACTS 4
 
-/* Task constants (tasks/reach.py:10-25, push.py:10-27, pick_and_place.py:11-29) */
+/* Cylinder proxies (Slide, pybullet.py:628-663 -> GEOM_CYLINDER): each cap's
+ * rim is sampled at PM_CYL_RIM_POINTS angles, listed so that every prefix of
+ * four is symmetric (0, 180, 90, 270 deg, then the diagonals) -- contacts
+ * with the ground take the first PM_MAX_GROUND_CONTACTS in this order, bottom
+ * cap first. */
+#define PM_CYL_RIM_POINTS 8
+#define PM_CYL_RIM_ORDER {0, 4, 2, 6, 1, 5, 3, 7}
+/* object-object contacts (Stack): vertices of object 1 against object 2, then
+ * of object 2 against object 1, the first PM_MAX_PAIR_CONTACTS within the
+ * margin */
+#define PM_MAX_PAIR_CONTACTS 4
+#define PM_CONTACT_MARGIN_PAIR 0.005
+/* tolerance of the box-box face tests (axis ties, face extents), metres */
+#define PM_PAIR_AXIS_TOL 1e-6
+
+/* Task constants: reach.py:10-25, push.py:10-27, pick_and_place.py:11-29,
+ * slide.py:10-29, stack.py:10-27, flip.py:12-24; episode lengths
+ * panda_gym/__init__.py:18-46 */
 #define PM_DISTANCE_THRESHOLD 0.05
+#define PM_STACK_DISTANCE_THRESHOLD 0.1
+#define PM_FLIP_DISTANCE_THRESHOLD 0.2
 #define PM_MAX_EPISODE_STEPS 50
+#define PM_STACK_MAX_EPISODE_STEPS 100
+#define PM_OBJECT_SIZE 0.04           /* push/pick_and_place/stack/flip object_size */
+#define PM_SLIDE_OBJECT_SIZE 0.06     /* slide.py:21: cylinder radius = height = 0.03 */
+#define PM_SLIDE_GOAL_X_OFFSET 0.4    /* slide.py:16 */
+#define PM_SLIDE_FRICTION 0.04        /* slide.py:41 lateral_friction */
+#define PM_SLIDE_TABLE_CX (-0.1)      /* slide.py:32: create_table(length=1.4, width=0.7, x_offset=-0.1) */
+#define PM_SLIDE_TABLE_HX 0.7
+#define PM_STACK_MASS1 2.0            /* stack.py:33-38 */
+#define PM_STACK_MASS2 1.0            /* stack.py:46-51 */
 
 #endif /* PANDA_MODEL_H */

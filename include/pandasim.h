@@ -29,28 +29,50 @@
 extern "C" {
 #endif
 
-#define PS_ABI_VERSION 1
+#define PS_ABI_VERSION 2
 
-enum { PS_TASK_REACH = 0, PS_TASK_PUSH = 1, PS_TASK_PICK_AND_PLACE = 2 };
+/* the six registered tasks (panda_gym/__init__.py:8-54) */
+enum {
+    PS_TASK_REACH = 0,
+    PS_TASK_PUSH = 1,
+    PS_TASK_PICK_AND_PLACE = 2,
+    PS_TASK_SLIDE = 3,
+    PS_TASK_STACK = 4,
+    PS_TASK_FLIP = 5,
+    PS_NUM_TASKS = 6
+};
 enum { PS_CONTROL_EE = 0, PS_CONTROL_JOINTS = 1 };
 enum { PS_REWARD_SPARSE = 0, PS_REWARD_DENSE = 1 };
+enum { PS_SHAPE_BOX = 0, PS_SHAPE_CYLINDER = 1 };
 enum { PS_OK = 0, PS_ERR_ARG = -1, PS_ERR_HIP = -2, PS_ERR_UNSUPPORTED = -3 };
 
 /* Scene/env configuration.  ps_default_config() fills the registered env
- * (panda_gym/__init__.py:8-54 + envs/panda_tasks.py:31-79); the scene flags
- * let tests build the reference's engine-level KAT scenes
- * (test/pybullet_test.py). */
+ * (panda_gym/__init__.py:8-54 + envs/panda_tasks.py:14-113 + the task's
+ * _create_scene); the scene fields let tests build the reference's
+ * engine-level KAT scenes (test/pybullet_test.py).
+ *   n_objects      dynamic objects: 0 (Reach), 1, or 2 (Stack)
+ *   object_shape   PS_SHAPE_BOX (half extents object_half) or
+ *                  PS_SHAPE_CYLINDER (radius object_half[0], half height
+ *                  object_half[2], axis z; slide.py:33-42)
+ *   object_mass    mass of object 1; object2_mass of object 2 (stack.py:33-55)
+ *   object_friction lateral friction of the objects (default 0.5; Slide 0.04)
+ *   table_cx/hx/hy table centre x and half extents (top at z = 0;
+ *                  pybullet.py:741-771) */
 typedef struct {
     int32_t task, control, reward, block_gripper;
-    int32_t has_table, has_plane, has_cube, reserved;
+    int32_t has_table, has_plane, n_objects, object_shape;
     float base[3];
-    float cube_half, cube_mass;
+    float object_half[3];
+    float object_mass, object2_mass, object_friction;
+    float table_cx, table_hx, table_hy;
 } ps_config;
 
 /* State layout: byte offsets from the state pointer.  Float fields are rows
- * of `stride` floats (env i at [row*stride + i]); goal is 3 rows of doubles,
- * rng is 4 rows of uint64 (PCG64 state hi, lo, inc hi, lo), elapsed one row
- * of int32 (TimeLimit counter). */
+ * of `stride` floats (env i at [row*stride + i]); goal is PS_MAX_GOAL_DIM
+ * rows of doubles, rng is 5 rows of uint64 (PCG64 state hi, lo, inc hi, lo of
+ * the task's np_random, then the splitmix64 state of Flip's goal stream),
+ * elapsed one row of int32 (TimeLimit counter). */
+#define PS_MAX_GOAL_DIM 6
 enum {
     PS_F_Q = 0,        /* 9 joint positions (DoF order: joints 0..6, 9, 10) */
     PS_F_QD = 9,       /* 9 joint velocities */
@@ -63,7 +85,12 @@ enum {
     PS_F_CQUAT = 66,   /* 4 object orientation quaternion x,y,z,w */
     PS_F_CVEL = 70,    /* 3 object linear velocity */
     PS_F_COMG = 73,    /* 3 object angular velocity */
-    PS_NUM_FLOAT_ROWS = 76
+    PS_F_C2POS = 76,   /* object 2 (Stack): position, */
+    PS_F_C2QUAT = 79,  /*   orientation, */
+    PS_F_C2VEL = 83,   /*   linear velocity, */
+    PS_F_C2OMG = 86,   /*   angular velocity */
+    PS_NUM_FLOAT_ROWS = 89,
+    PS_NUM_RNG_ROWS = 5
 };
 
 typedef struct {
@@ -85,6 +112,8 @@ void ps_destroy(ps_ctx *ctx);
 const char *ps_last_error(const ps_ctx *ctx);
 int ps_obs_dim(const ps_ctx *ctx);
 int ps_action_dim(const ps_ctx *ctx);
+int ps_goal_dim(const ps_ctx *ctx);        /* 3, 4 (Flip quaternion) or 6 (Stack) */
+int ps_max_episode_steps(const ps_ctx *ctx); /* TimeLimit: 50, Stack 100 (__init__.py:18-46) */
 
 /* Zero state, identity object orientation and PyBullet's default joint
  * velocity motors (loadURDF, core.py:40-52). */
@@ -101,7 +130,7 @@ int ps_reset(ps_ctx *ctx, void *state, const uint8_t *mask, const uint64_t *seed
  * Panda.set_action (panda.py:52-107, incl. calculateInverseKinematics) ->
  * PyBullet.step (pybullet.py:52-55, 20 substeps) -> _get_obs -> is_success /
  * compute_reward.  actions: [B, action_dim] f32.  obs [B, obs_dim], ag/dg
- * [B,3], reward [B] f32, terminated/truncated [B] u8.  autoreset != 0:
+ * [B, goal_dim], reward [B] f32, terminated/truncated [B] u8.  autoreset != 0:
  * finished envs are reset in-kernel (generator continues) and obs/ag/dg hold
  * the reset observation; final_obs/final_ag (may be NULL) receive the
  * pre-reset observation of every env. */
@@ -139,20 +168,28 @@ int ps_rng_seed(ps_ctx *ctx, void *state, const uint8_t *mask, const uint64_t *s
 int ps_rng_uniform(ps_ctx *ctx, void *state, const uint8_t *mask, int n, const double *low, const double *high,
                    double *out, void *stream);
 
-/* getBasePositionAndOrientation / getEulerFromQuaternion / getBaseVelocity of
- * the object body (pybullet.py:284-349): pos, euler, lin_vel, ang_vel [B,3],
- * quat [B,4] (x,y,z,w); any output may be NULL.  PS_ERR_UNSUPPORTED if the
- * scene has no object. */
-int ps_base_state(ps_ctx *ctx, const void *state, float *pos, float *quat, float *euler, float *lin_vel,
-                  float *ang_vel, void *stream);
+/* Flip's goal, scipy Rotation.random().as_quat() (flip.py:70-72): the
+ * reference draws it from numpy's unseeded global RandomState; here from each
+ * masked env's splitmix64 goal stream (seeded with the env seed by ps_reset /
+ * ps_rng_seed), four Box-Muller normals normalised, into out [B, 4] f64. */
+int ps_rng_rotation(ps_ctx *ctx, void *state, const uint8_t *mask, double *out, void *stream);
 
-/* Task.compute_reward / is_success (reach.py:56-65, push.py:89-98),
- * vectorised for HER (core.py:226): n goal pairs [n,3], each f64 when its
- * *_is_double flag is set, else f32.  As numpy does, the distance is computed
- * in f64 when either side is f64 and in f32 (threshold 0.05f) when both are
- * f32.  reward and success may be NULL. */
-int ps_compute_reward(int reward_type, const void *ag, int ag_is_double, const void *dg, int dg_is_double,
-                      float *reward, uint8_t *success, int64_t n, void *stream);
+/* getBasePositionAndOrientation / getEulerFromQuaternion / getBaseVelocity of
+ * object `object` (0 or 1) (pybullet.py:284-349): pos, euler, lin_vel, ang_vel
+ * [B,3], quat [B,4] (x,y,z,w); any output may be NULL.  PS_ERR_UNSUPPORTED if
+ * the scene has no such object. */
+int ps_base_state(ps_ctx *ctx, const void *state, int object, float *pos, float *quat, float *euler,
+                  float *lin_vel, float *ang_vel, void *stream);
+
+/* Task.compute_reward / is_success of `task` (reach.py:56-65, push.py:89-98,
+ * stack.py:118-131, flip.py:80-91), vectorised for HER (core.py:226): n goal
+ * pairs [n, goal_dim(task)], each f64 when its *_is_double flag is set, else
+ * f32.  Goal-distance tasks use utils.distance (threshold 0.05, Stack 0.1),
+ * Flip uses utils.angle_distance = 1 - <a, b>^2 (threshold 0.2).  As numpy
+ * does, the arithmetic is f64 when either side is f64 and f32 (threshold
+ * rounded to f32) when both are f32.  reward and success may be NULL. */
+int ps_compute_reward(int task, int reward_type, const void *ag, int ag_is_double, const void *dg,
+                      int dg_is_double, float *reward, uint8_t *success, int64_t n, void *stream);
 
 #ifdef __cplusplus
 }

@@ -15,15 +15,22 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "libpanda_oracle.so")
 
-TASKS = {"reach": 0, "push": 1, "pick_and_place": 2}
+TASKS = {"reach": 0, "push": 1, "pick_and_place": 2, "slide": 3, "stack": 4, "flip": 5}
 
 
 class Config(C.Structure):
     _fields_ = [
         ("task", C.c_int32), ("control", C.c_int32), ("reward", C.c_int32), ("block_gripper", C.c_int32),
-        ("has_table", C.c_int32), ("has_plane", C.c_int32), ("has_cube", C.c_int32), ("has_robot", C.c_int32),
-        ("base", C.c_double * 3), ("cube_half", C.c_double), ("cube_mass", C.c_double),
+        ("has_table", C.c_int32), ("has_plane", C.c_int32), ("n_objects", C.c_int32), ("object_shape", C.c_int32),
+        ("has_robot", C.c_int32), ("reserved", C.c_int32),
+        ("base", C.c_double * 3), ("object_half", C.c_double * 3),
+        ("object_mass", C.c_double), ("object2_mass", C.c_double), ("object_friction", C.c_double),
+        ("table_cx", C.c_double), ("table_hx", C.c_double), ("table_hy", C.c_double),
     ]
+
+
+class Body(C.Structure):
+    _fields_ = [("pos", C.c_double * 3), ("quat", C.c_double * 4), ("vel", C.c_double * 3), ("omg", C.c_double * 3)]
 
 
 class Env(C.Structure):
@@ -31,8 +38,7 @@ class Env(C.Structure):
         ("q", C.c_double * 9), ("qd", C.c_double * 9),
         ("m_target", C.c_double * 9), ("m_kp", C.c_double * 9), ("m_kd", C.c_double * 9),
         ("m_vel", C.c_double * 9), ("m_maximp", C.c_double * 9),
-        ("cpos", C.c_double * 3), ("cquat", C.c_double * 4), ("cvel", C.c_double * 3), ("comg", C.c_double * 3),
-        ("goal", C.c_double * 3), ("elapsed", C.c_int64), ("rng", C.c_uint64 * 4),
+        ("obj", Body * 2), ("goal", C.c_double * 6), ("elapsed", C.c_int64), ("rng", C.c_uint64 * 5),
     ]
 
 
@@ -66,14 +72,17 @@ def lib():
         L.po_euler_from_quaternion.argtypes = [P(D), P(D)]
         L.po_obs_dim.argtypes = [P(Config)]
         L.po_action_dim.argtypes = [P(Config)]
+        L.po_goal_dim.argtypes = [P(Config)]
+        L.po_max_episode_steps.argtypes = [P(Config)]
+        L.po_flip_goal.argtypes = [P(C.c_uint64), P(D)]
         F, U8 = P(C.c_float), P(C.c_uint8)
         L.po_reset.argtypes = [P(Config), P(Env), I, C.c_uint64, F, F, F]
         L.po_get_obs.argtypes = [P(Config), P(Env), F, F, F]
         L.po_step.argtypes = [P(Config), P(Env), F, F, F, F, F, U8, U8, I, F, F, P(Stats)]
         L.po_step_batch.argtypes = [P(Config), P(Env), I, F, F, F, F, F, U8, U8, I, P(Stats)]
-        L.po_compute_reward.argtypes = [I, F, P(D)]
+        L.po_compute_reward.argtypes = [I, I, F, P(D)]
         L.po_compute_reward.restype = C.c_float
-        L.po_is_success.argtypes = [F, P(D)]
+        L.po_is_success.argtypes = [I, F, P(D)]
         L.po_is_success.restype = C.c_uint8
         L.po_pcg64_seed.argtypes = [C.c_uint64, P(C.c_uint64)]
         L.po_pcg64_next.argtypes = [P(C.c_uint64)]
@@ -100,9 +109,9 @@ def config(task="reach", control="ee", reward="sparse", **overrides) -> Config:
     cfg = Config()
     lib().po_default_config(C.byref(cfg), TASKS[task], 0 if control == "ee" else 1, 0 if reward == "sparse" else 1)
     for k, v in overrides.items():
-        if k == "base":
+        if k in ("base", "object_half"):
             for i in range(3):
-                cfg.base[i] = v[i]
+                getattr(cfg, k)[i] = v[i]
         else:
             setattr(cfg, k, v)
     return cfg
@@ -153,26 +162,34 @@ def action_dim(cfg) -> int:
     return lib().po_action_dim(C.byref(cfg))
 
 
+def goal_dim(cfg) -> int:
+    return lib().po_goal_dim(C.byref(cfg))
+
+
+def max_episode_steps(cfg) -> int:
+    return lib().po_max_episode_steps(C.byref(cfg))
+
+
 def reset(cfg, env, seed=None):
-    od = obs_dim(cfg)
-    obs, ag, dg = np.zeros(od, np.float32), np.zeros(3, np.float32), np.zeros(3, np.float32)
+    od, gd = obs_dim(cfg), goal_dim(cfg)
+    obs, ag, dg = np.zeros(od, np.float32), np.zeros(gd, np.float32), np.zeros(gd, np.float32)
     lib().po_reset(C.byref(cfg), C.byref(env), 0 if seed is None else 1, 0 if seed is None else int(seed),
                    _fp(obs), _fp(ag), _fp(dg))
     return obs, ag, dg
 
 
 def get_obs(cfg, env):
-    od = obs_dim(cfg)
-    obs, ag, dg = np.zeros(od, np.float32), np.zeros(3, np.float32), np.zeros(3, np.float32)
+    od, gd = obs_dim(cfg), goal_dim(cfg)
+    obs, ag, dg = np.zeros(od, np.float32), np.zeros(gd, np.float32), np.zeros(gd, np.float32)
     lib().po_get_obs(C.byref(cfg), C.byref(env), _fp(obs), _fp(ag), _fp(dg))
     return obs, ag, dg
 
 
 def step(cfg, env, action, autoreset=False, stats: Stats | None = None):
-    od = obs_dim(cfg)
+    od, gd = obs_dim(cfg), goal_dim(cfg)
     a = np.ascontiguousarray(action, dtype=np.float32)
-    obs, ag, dg = np.zeros(od, np.float32), np.zeros(3, np.float32), np.zeros(3, np.float32)
-    fo, fa = np.zeros(od, np.float32), np.zeros(3, np.float32)
+    obs, ag, dg = np.zeros(od, np.float32), np.zeros(gd, np.float32), np.zeros(gd, np.float32)
+    fo, fa = np.zeros(od, np.float32), np.zeros(gd, np.float32)
     r = np.zeros(1, np.float32)
     te, tr = np.zeros(1, np.uint8), np.zeros(1, np.uint8)
     lib().po_step(C.byref(cfg), C.byref(env), _fp(a), _fp(obs), _fp(ag), _fp(dg), _fp(r),
@@ -181,16 +198,24 @@ def step(cfg, env, action, autoreset=False, stats: Stats | None = None):
     return obs, ag, dg, float(r[0]), bool(te[0]), bool(tr[0])
 
 
-def compute_reward(reward_type: str, ag, dg):
+def compute_reward(reward_type: str, ag, dg, task: str = "push"):
     a = np.ascontiguousarray(ag, dtype=np.float32)
     d = np.ascontiguousarray(dg, dtype=np.float64)
-    return lib().po_compute_reward(0 if reward_type == "sparse" else 1, _fp(a), _dp(d))
+    return lib().po_compute_reward(TASKS[task], 0 if reward_type == "sparse" else 1, _fp(a), _dp(d))
 
 
-def is_success(ag, dg) -> bool:
+def is_success(ag, dg, task: str = "push") -> bool:
     a = np.ascontiguousarray(ag, dtype=np.float32)
     d = np.ascontiguousarray(dg, dtype=np.float64)
-    return bool(lib().po_is_success(_fp(a), _dp(d)))
+    return bool(lib().po_is_success(TASKS[task], _fp(a), _dp(d)))
+
+
+def flip_goal(aux_state: int):
+    """(new aux state, quaternion) of the Flip goal stream."""
+    st = (C.c_uint64 * 1)(aux_state)
+    q = np.zeros(4)
+    lib().po_flip_goal(st, _dp(q))
+    return int(st[0]), q
 
 
 def pcg64_seed(seed: int) -> np.ndarray:

@@ -490,9 +490,15 @@ void po_inverse_kinematics(const po_config *cfg, const double q_start[9], int li
 }
 
 /* ---------------------------------------------------------- constraints */
-#define ND 15 /* robot 9 + cube [omega(3), v(3)], world frame */
-#define MAX_ROWS 128
-#define MAX_CONTACTS 32
+/* velocity DoFs: robot 9, then per object [omega(3), v(3)], world frame */
+#define ND (9 + 6 * PO_MAX_OBJECTS)
+#define MAX_ROWS 160
+#define MAX_CONTACTS 48
+#define OBJ_DOF(i) (9 + 6 * (i))
+#define BODY_STATIC (-1)
+#define BODY_OBJ(i) (-2 - (i)) /* object i */
+#define IS_OBJ(b) ((b) <= -2)
+#define OBJ_OF(b) (-2 - (b))
 
 typedef struct {
     double J[ND], MJ[ND];
@@ -501,10 +507,48 @@ typedef struct {
 } orow;
 
 typedef struct {
-    int bodyA; /* robot link index, or -2 = cube */
-    int bodyB; /* -2 = cube, -1 = static */
+    int bodyA; /* robot link index or BODY_OBJ(i) */
+    int bodyB; /* BODY_OBJ(i) or BODY_STATIC */
     double pA[3], pB[3], n[3], dist, mu;
 } ocontact;
+
+/* per-substep object quantities */
+typedef struct {
+    double R[9], Iinv[9], inv_m, I[3], mass;
+    int iso; /* isotropic inertia (cubes): Iinv = I^-1 * identity exactly */
+} oobj;
+
+/* btBoxShape / btCylinderShapeZ::calculateLocalInertia (createMultiBody
+ * computes the base inertia from the collision shape, pybullet.py:709-724) */
+static void object_inertia(const po_config *cfg, int i, double I[3], double *mass) {
+    double m = i == 0 ? cfg->object_mass : cfg->object2_mass;
+    const double *h = cfg->object_half;
+    *mass = m;
+    if (cfg->object_shape == PO_SHAPE_CYLINDER) {
+        double r = h[0], hh = h[2];
+        double t1 = m / 12.0 * (4.0 * hh * hh) + m / 4.0 * (r * r), t2 = m / 2.0 * (r * r);
+        I[0] = t1; I[1] = t1; I[2] = t2;
+    } else {
+        double lx = 2.0 * h[0], ly = 2.0 * h[1], lz = 2.0 * h[2];
+        I[0] = m / 12.0 * (ly * ly + lz * lz);
+        I[1] = m / 12.0 * (lx * lx + lz * lz);
+        I[2] = m / 12.0 * (lx * lx + ly * ly);
+    }
+}
+
+static void object_setup(const po_config *cfg, const po_env *env, int i, oobj *o) {
+    object_inertia(cfg, i, o->I, &o->mass);
+    o->inv_m = 1.0 / o->mass;
+    quat_to_mat(env->obj[i].quat, o->R);
+    o->iso = o->I[0] == o->I[1] && o->I[1] == o->I[2];
+    if (o->iso) {
+        memset(o->Iinv, 0, sizeof o->Iinv);
+        o->Iinv[0] = o->Iinv[4] = o->Iinv[8] = 1.0 / o->I[0];
+    } else {
+        double Ii[3] = {1.0 / o->I[0], 1.0 / o->I[1], 1.0 / o->I[2]};
+        inertia_world(o->R, Ii, o->Iinv);
+    }
+}
 
 /* btPlaneSpace1 */
 static void plane_space(const double n[3], double p[3], double q[3]) {
@@ -520,7 +564,7 @@ static void plane_space(const double n[3], double p[3], double q[3]) {
 }
 
 static int ground_top(const po_config *cfg, double x, double y, double *top) {
-    if (cfg->has_table && fabs(x - PM_TABLE_CX) <= PM_TABLE_HX && fabs(y) <= PM_TABLE_HY) {
+    if (cfg->has_table && fabs(x - cfg->table_cx) <= cfg->table_hx && fabs(y) <= cfg->table_hy) {
         *top = PM_TABLE_TOP;
         return 1;
     }
@@ -531,17 +575,209 @@ static int ground_top(const po_config *cfg, double x, double y, double *top) {
     return 0;
 }
 
+/* contact candidates of an object against the ground, object frame:
+ * box vertices (index bits = signs of x, y, z) or cylinder rim points (bottom
+ * cap, then top cap, each in PM_CYL_RIM_ORDER) */
+static int object_support_points(const po_config *cfg, double pts[][3]) {
+    const double *h = cfg->object_half;
+    if (cfg->object_shape == PO_SHAPE_CYLINDER) {
+        static const int order[PM_CYL_RIM_POINTS] = PM_CYL_RIM_ORDER;
+        int n = 0;
+        for (int cap = 0; cap < 2; cap++)
+            for (int j = 0; j < PM_CYL_RIM_POINTS; j++) {
+                double th = order[j] * (2.0 * 3.14159265358979323846 / PM_CYL_RIM_POINTS);
+                pts[n][0] = h[0] * cos(th);
+                pts[n][1] = h[0] * sin(th);
+                pts[n][2] = cap ? h[2] : -h[2];
+                n++;
+            }
+        return n;
+    }
+    for (int v = 0; v < 8; v++) {
+        pts[v][0] = (v & 1) ? h[0] : -h[0];
+        pts[v][1] = (v & 2) ? h[1] : -h[1];
+        pts[v][2] = (v & 4) ? h[2] : -h[2];
+    }
+    return 8;
+}
+
+/* Closest point of the object's solid to the local point `loc`: cl (surface
+ * point), nl (outward unit normal at cl), return value = signed distance of
+ * loc from the surface (negative inside). */
+static double object_closest(const po_config *cfg, const double loc[3], double cl[3], double nl[3]) {
+    const double *h = cfg->object_half;
+    if (cfg->object_shape == PO_SHAPE_CYLINDER) {
+        double r = h[0], hh = h[2];
+        double rho = sqrt(loc[0] * loc[0] + loc[1] * loc[1]);
+        double zc = loc[2] < -hh ? -hh : (loc[2] > hh ? hh : loc[2]);
+        double s = rho > r ? r / rho : 1.0;
+        cl[0] = loc[0] * s; cl[1] = loc[1] * s; cl[2] = zc;
+        double dif[3] = {loc[0] - cl[0], loc[1] - cl[1], loc[2] - cl[2]};
+        double dn = v3_norm(dif);
+        if (dn > 1e-9) {
+            for (int d = 0; d < 3; d++) nl[d] = dif[d] / dn;
+            return dn;
+        }
+        double side = r - rho, cap = hh - fabs(loc[2]);
+        if (side < cap) {
+            if (rho > 1e-12) { nl[0] = loc[0] / rho; nl[1] = loc[1] / rho; }
+            else { nl[0] = 1.0; nl[1] = 0.0; }
+            nl[2] = 0.0;
+            cl[0] = nl[0] * r; cl[1] = nl[1] * r;
+            return -side;
+        }
+        nl[0] = nl[1] = 0.0;
+        nl[2] = loc[2] >= 0.0 ? 1.0 : -1.0;
+        cl[2] = nl[2] * hh;
+        return -cap;
+    }
+    double dif[3];
+    for (int d = 0; d < 3; d++) {
+        cl[d] = loc[d] < -h[d] ? -h[d] : (loc[d] > h[d] ? h[d] : loc[d]);
+        dif[d] = loc[d] - cl[d];
+    }
+    double dn = v3_norm(dif);
+    if (dn > 1e-9) {
+        for (int d = 0; d < 3; d++) nl[d] = dif[d] / dn;
+        return dn;
+    }
+    int ax = 0;
+    double best = h[0] - fabs(loc[0]);
+    for (int d = 1; d < 3; d++)
+        if (h[d] - fabs(loc[d]) < best) { best = h[d] - fabs(loc[d]); ax = d; }
+    nl[0] = nl[1] = nl[2] = 0.0;
+    nl[ax] = loc[ax] >= 0.0 ? 1.0 : -1.0;
+    cl[ax] = nl[ax] * h[ax];
+    return -best;
+}
+
+/* Box-box contacts of the two objects (Stack; Bullet's btBoxBoxDetector,
+ * restated with face axes only):
+ *   1. separating-axis test over the six face normals; the axis of least
+ *      penetration (ties keep the earlier axis, PM_PAIR_AXIS_TOL) gives the
+ *      reference box R and the normal n from R toward the incident box I;
+ *   2. I's face most opposed to n is clipped against R's reference face
+ *      rectangle (Sutherland-Hodgman in the face's 2-D frame, depths
+ *      interpolated along the clipped edges);
+ *   3. clipped points closer than the margin are contacts (A = I at its
+ *      face point, B = R at the projection on its face); more than
+ *      PM_MAX_PAIR_CONTACTS are thinned to evenly spaced polygon vertices. */
+typedef struct {
+    double u, v, depth;
+} oclip;
+
+static int clip_half(const oclip *in, int n, int axis, double sign, double lim, oclip *out) {
+    /* keep points with sign * coord <= lim */
+    int m = 0;
+    for (int i = 0; i < n; i++) {
+        const oclip *a = &in[i], *b = &in[(i + 1) % n];
+        double ca = sign * (axis == 0 ? a->u : a->v) - lim, cb = sign * (axis == 0 ? b->u : b->v) - lim;
+        if (ca <= 0.0) out[m++] = *a;
+        if ((ca < 0.0 && cb > 0.0) || (ca > 0.0 && cb < 0.0)) {
+            double t = ca / (ca - cb);
+            out[m].u = a->u + t * (b->u - a->u);
+            out[m].v = a->v + t * (b->v - a->v);
+            out[m].depth = a->depth + t * (b->depth - a->depth);
+            m++;
+        }
+    }
+    return m;
+}
+
+static void box_box_contacts(const po_config *cfg, const po_env *env, const oobj *ob, ocontact *out, int *nc) {
+    const double *h = cfg->object_half;
+    double d[3];
+    for (int k = 0; k < 3; k++) d[k] = env->obj[1].pos[k] - env->obj[0].pos[k];
+    double best = 1e30, nref[3] = {0, 0, 0};
+    int ref = 0, axn = 0;
+    for (int b = 0; b < 2; b++)
+        for (int ax = 0; ax < 3; ax++) {
+            double L[3] = {ob[b].R[ax], ob[b].R[3 + ax], ob[b].R[6 + ax]};
+            double ra = 0.0, rb = 0.0;
+            for (int k = 0; k < 3; k++) {
+                ra += h[k] * fabs(ob[0].R[k] * L[0] + ob[0].R[3 + k] * L[1] + ob[0].R[6 + k] * L[2]);
+                rb += h[k] * fabs(ob[1].R[k] * L[0] + ob[1].R[3 + k] * L[1] + ob[1].R[6 + k] * L[2]);
+            }
+            double c = v3_dot(d, L);
+            double pen = ra + rb - fabs(c);
+            if (pen < -PM_CONTACT_MARGIN_PAIR) return; /* separated */
+            if (pen < best - PM_PAIR_AXIS_TOL) {
+                best = pen;
+                ref = b;
+                axn = ax;
+                double sg = (b == 0 ? c : -c) >= 0.0 ? 1.0 : -1.0; /* from R toward I */
+                for (int k = 0; k < 3; k++) nref[k] = L[k] * sg;
+            }
+        }
+    int inc = 1 - ref;
+    const double *cr = env->obj[ref].pos, *ci = env->obj[inc].pos;
+    /* reference face frame: centre cf, tangents t1, t2 (R's other two axes) */
+    int a1 = (axn + 1) % 3, a2 = (axn + 2) % 3;
+    double t1[3] = {ob[ref].R[a1], ob[ref].R[3 + a1], ob[ref].R[6 + a1]};
+    double t2[3] = {ob[ref].R[a2], ob[ref].R[3 + a2], ob[ref].R[6 + a2]};
+    double cf[3];
+    for (int k = 0; k < 3; k++) cf[k] = cr[k] + nref[k] * h[axn];
+    /* incident face: I's axis most anti-parallel to n */
+    int ai = 0;
+    double mostneg = 2.0, si = 1.0;
+    for (int ax = 0; ax < 3; ax++) {
+        double L[3] = {ob[inc].R[ax], ob[inc].R[3 + ax], ob[inc].R[6 + ax]};
+        double dn = v3_dot(L, nref);
+        if (-fabs(dn) < mostneg) { mostneg = -fabs(dn); ai = ax; si = dn > 0.0 ? -1.0 : 1.0; }
+    }
+    int b1 = (ai + 1) % 3, b2 = (ai + 2) % 3;
+    oclip poly[16], tmp[16];
+    static const double cu[4] = {-1, 1, 1, -1}, cv[4] = {-1, -1, 1, 1};
+    for (int k = 0; k < 4; k++) {
+        double loc[3];
+        loc[ai] = si * h[ai];
+        loc[b1] = cu[k] * h[b1];
+        loc[b2] = cv[k] * h[b2];
+        double pw[3], rel[3];
+        m3_vec(ob[inc].R, loc, pw);
+        for (int j = 0; j < 3; j++) rel[j] = pw[j] + ci[j] - cf[j];
+        poly[k].u = v3_dot(rel, t1);
+        poly[k].v = v3_dot(rel, t2);
+        poly[k].depth = v3_dot(rel, nref);
+    }
+    int n = 4;
+    n = clip_half(poly, n, 0, 1.0, h[a1], tmp);
+    n = clip_half(tmp, n, 0, -1.0, h[a1], poly);
+    n = clip_half(poly, n, 1, 1.0, h[a2], tmp);
+    n = clip_half(tmp, n, 1, -1.0, h[a2], poly);
+    oclip keep[16];
+    int m = 0;
+    for (int k = 0; k < n; k++)
+        if (poly[k].depth < PM_CONTACT_MARGIN_PAIR) keep[m++] = poly[k];
+    int take = m < PM_MAX_PAIR_CONTACTS ? m : PM_MAX_PAIR_CONTACTS;
+    for (int k = 0; k < take; k++) {
+        const oclip *p = &keep[m <= PM_MAX_PAIR_CONTACTS ? k : (k * m) / PM_MAX_PAIR_CONTACTS];
+        ocontact *c = &out[(*nc)++];
+        c->bodyA = BODY_OBJ(inc);
+        c->bodyB = BODY_OBJ(ref);
+        memcpy(c->n, nref, sizeof nref);
+        for (int j = 0; j < 3; j++) {
+            c->pB[j] = cf[j] + p->u * t1[j] + p->v * t2[j];
+            c->pA[j] = c->pB[j] + nref[j] * p->depth;
+        }
+        c->dist = p->depth;
+        c->mu = cfg->object_friction * cfg->object_friction;
+    }
+}
+
 /* Contact generation (replaces Bullet's broadphase + box-box / convex
  * narrowphase with the proxies of panda_model.h), fixed order and caps:
- *   1. cube vertices vs ground (table top or plane): the first
- *      PM_MAX_GROUND_CONTACTS vertices (index order) within the margin
- *   2. gripper spheres vs cube (closest point on the cube)
- *   3. gripper spheres vs ground
- *   2+3 share PM_MAX_ROBOT_CONTACTS slots, filled in that order. */
-static int gen_contacts(const po_config *cfg, const po_env *env, const okin *k, ocontact *out) {
+ *   1. per object: support points (box vertices / cylinder rim points) vs
+ *      ground (table top or plane): the first PM_MAX_GROUND_CONTACTS within
+ *      the margin, in candidate order
+ *   2. object-object (Stack): box_box_contacts
+ *   3. gripper spheres vs object 1, vs object 2 (closest point on the solid)
+ *   4. gripper spheres vs ground
+ *   3+4 share PM_MAX_ROBOT_CONTACTS slots, filled in that order.
+ * Friction coefficients are products of the two bodies' lateral frictions
+ * (objects: object_friction, ground/table: 0.5, gripper spheres: their own). */
+static int gen_contacts(const po_config *cfg, const po_env *env, const okin *k, const oobj *ob, ocontact *out) {
     int nc = 0;
-    double Rc[9];
-    if (cfg->has_cube) quat_to_mat(env->cquat, Rc);
     double sc[PM_NUM_SPHERES][3];
     if (cfg->has_robot)
         for (int s = 0; s < PM_NUM_SPHERES; s++) {
@@ -549,72 +785,57 @@ static int gen_contacts(const po_config *cfg, const po_env *env, const okin *k, 
             m3_vec(k->R[SPH[s].link], SPH[s].c, t);
             for (int d = 0; d < 3; d++) sc[s][d] = k->o[SPH[s].link][d] + t[d];
         }
-    if (cfg->has_cube) {
-        double h = cfg->cube_half;
+    double pts[2 * PM_CYL_RIM_POINTS][3];
+    int npts = object_support_points(cfg, pts);
+    for (int i = 0; i < cfg->n_objects; i++) {
+        const po_body *b = &env->obj[i];
         int ng = 0;
-        for (int v = 0; v < 8 && ng < PM_MAX_GROUND_CONTACTS; v++) {
-            double loc[3] = {(v & 1) ? h : -h, (v & 2) ? h : -h, (v & 4) ? h : -h}, pw[3];
-            m3_vec(Rc, loc, pw);
-            for (int d = 0; d < 3; d++) pw[d] += env->cpos[d];
+        for (int v = 0; v < npts && ng < PM_MAX_GROUND_CONTACTS; v++) {
+            double pw[3];
+            m3_vec(ob[i].R, pts[v], pw);
+            for (int d = 0; d < 3; d++) pw[d] += b->pos[d];
             double top;
             if (!ground_top(cfg, pw[0], pw[1], &top)) continue;
             double dist = pw[2] - top;
             if (dist < PM_CONTACT_MARGIN_GROUND) {
                 ocontact *c = &out[nc++];
                 ng++;
-                c->bodyA = -2;
-                c->bodyB = -1;
+                c->bodyA = BODY_OBJ(i);
+                c->bodyB = BODY_STATIC;
                 c->n[0] = 0; c->n[1] = 0; c->n[2] = 1;
                 memcpy(c->pA, pw, sizeof pw);
                 c->pB[0] = pw[0]; c->pB[1] = pw[1]; c->pB[2] = top;
                 c->dist = dist;
-                c->mu = PM_DEFAULT_FRICTION * PM_DEFAULT_FRICTION;
+                c->mu = cfg->object_friction * PM_DEFAULT_FRICTION;
             }
         }
     }
+    if (cfg->n_objects == 2) box_box_contacts(cfg, env, ob, out, &nc);
     int nr = 0;
-    if (cfg->has_cube && cfg->has_robot) {
-        double h = cfg->cube_half;
-        for (int s = 0; s < PM_NUM_SPHERES && nr < PM_MAX_ROBOT_CONTACTS; s++) {
-            double rel[3] = {sc[s][0] - env->cpos[0], sc[s][1] - env->cpos[1], sc[s][2] - env->cpos[2]}, loc[3];
-            m3_tvec(Rc, rel, loc);
-            double cl[3], dif[3], nl[3], dist;
-            for (int d = 0; d < 3; d++) {
-                cl[d] = loc[d] < -h ? -h : (loc[d] > h ? h : loc[d]);
-                dif[d] = loc[d] - cl[d];
-            }
-            double dn = v3_norm(dif);
-            if (dn > 1e-9) {
-                for (int d = 0; d < 3; d++) nl[d] = dif[d] / dn;
-                dist = dn - SPH[s].r;
-            } else {
-                int ax = 0;
-                double best = h - fabs(loc[0]);
-                for (int d = 1; d < 3; d++)
-                    if (h - fabs(loc[d]) < best) { best = h - fabs(loc[d]); ax = d; }
-                nl[0] = nl[1] = nl[2] = 0.0;
-                nl[ax] = loc[ax] >= 0.0 ? 1.0 : -1.0;
-                cl[ax] = nl[ax] * h;
-                dist = -best - SPH[s].r;
-            }
-            if (dist < PM_CONTACT_MARGIN_SPHERE) {
-                ocontact *c = &out[nc++];
-                nr++;
-                c->bodyA = SPH[s].link;
-                c->bodyB = -2;
-                m3_vec(Rc, nl, c->n);
-                double pw[3];
-                m3_vec(Rc, cl, pw);
-                for (int d = 0; d < 3; d++) {
-                    c->pB[d] = env->cpos[d] + pw[d];
-                    c->pA[d] = sc[s][d] - c->n[d] * SPH[s].r;
-                }
-                c->dist = dist;
-                c->mu = SPH[s].mu * PM_DEFAULT_FRICTION;
-            }
-        }
-    }
     if (cfg->has_robot) {
+        for (int i = 0; i < cfg->n_objects; i++)
+            for (int s = 0; s < PM_NUM_SPHERES && nr < PM_MAX_ROBOT_CONTACTS; s++) {
+                const po_body *b = &env->obj[i];
+                double rel[3] = {sc[s][0] - b->pos[0], sc[s][1] - b->pos[1], sc[s][2] - b->pos[2]}, loc[3];
+                m3_tvec(ob[i].R, rel, loc);
+                double cl[3], nl[3];
+                double dist = object_closest(cfg, loc, cl, nl) - SPH[s].r;
+                if (dist < PM_CONTACT_MARGIN_SPHERE) {
+                    ocontact *c = &out[nc++];
+                    nr++;
+                    c->bodyA = SPH[s].link;
+                    c->bodyB = BODY_OBJ(i);
+                    m3_vec(ob[i].R, nl, c->n);
+                    double pw[3];
+                    m3_vec(ob[i].R, cl, pw);
+                    for (int d = 0; d < 3; d++) {
+                        c->pB[d] = b->pos[d] + pw[d];
+                        c->pA[d] = sc[s][d] - c->n[d] * SPH[s].r;
+                    }
+                    c->dist = dist;
+                    c->mu = SPH[s].mu * cfg->object_friction;
+                }
+            }
         for (int s = 0; s < PM_NUM_SPHERES && nr < PM_MAX_ROBOT_CONTACTS; s++) {
             double top;
             if (!ground_top(cfg, sc[s][0], sc[s][1], &top)) continue;
@@ -623,7 +844,7 @@ static int gen_contacts(const po_config *cfg, const po_env *env, const okin *k, 
                 ocontact *c = &out[nc++];
                 nr++;
                 c->bodyA = SPH[s].link;
-                c->bodyB = -1;
+                c->bodyB = BODY_STATIC;
                 c->n[0] = 0; c->n[1] = 0; c->n[2] = 1;
                 c->pA[0] = sc[s][0]; c->pA[1] = sc[s][1]; c->pA[2] = sc[s][2] - SPH[s].r;
                 c->pB[0] = sc[s][0]; c->pB[1] = sc[s][1]; c->pB[2] = top;
@@ -646,12 +867,14 @@ static void contact_row_jac(const okin *k, const po_env *env, const ocontact *c,
             double Jv[3][9], Jw[3][9];
             point_jac(k, body, p, Jv, Jw);
             for (int d = 0; d < 9; d++) J[d] += sg * (n[0] * Jv[0][d] + n[1] * Jv[1][d] + n[2] * Jv[2][d]);
-        } else if (body == -2) {
-            double r[3] = {p[0] - env->cpos[0], p[1] - env->cpos[1], p[2] - env->cpos[2]}, rn[3];
+        } else if (IS_OBJ(body)) {
+            const double *x = env->obj[OBJ_OF(body)].pos;
+            int o = OBJ_DOF(OBJ_OF(body));
+            double r[3] = {p[0] - x[0], p[1] - x[1], p[2] - x[2]}, rn[3];
             v3_cross(r, n, rn);
             for (int d = 0; d < 3; d++) {
-                J[9 + d] += sg * rn[d];
-                J[12 + d] += sg * n[d];
+                J[o + d] += sg * rn[d];
+                J[o + 3 + d] += sg * n[d];
             }
         }
     }
@@ -697,15 +920,24 @@ static double solve_cone(orow *a, orow *b, double lam_n, double dv[ND]) {
     return fabs(ra) > fabs(rb) ? ra : rb;
 }
 
-static void finish_row(orow *r, const double Minv_r[81], double cube_inv_I, double cube_inv_m, const double v1[ND]) {
+static void finish_row(orow *r, const double Minv_r[81], const oobj *ob, int n_objects, const double v1[ND]) {
     for (int a = 0; a < 9; a++) {
         double s = 0.0;
         for (int b = 0; b < 9; b++) s += Minv_r[a * 9 + b] * r->J[b];
         r->MJ[a] = s;
     }
-    for (int d = 0; d < 3; d++) {
-        r->MJ[9 + d] = r->J[9 + d] * cube_inv_I;
-        r->MJ[12 + d] = r->J[12 + d] * cube_inv_m;
+    for (int i = 0; i < PO_MAX_OBJECTS; i++) {
+        int o = OBJ_DOF(i);
+        if (i >= n_objects) {
+            for (int d = 0; d < 6; d++) r->MJ[o + d] = 0.0;
+            continue;
+        }
+        if (ob[i].iso) {
+            for (int d = 0; d < 3; d++) r->MJ[o + d] = r->J[o + d] * ob[i].Iinv[0];
+        } else {
+            m3_vec(ob[i].Iinv, &r->J[o], &r->MJ[o]);
+        }
+        for (int d = 0; d < 3; d++) r->MJ[o + 3 + d] = r->J[o + 3 + d] * ob[i].inv_m;
     }
     double den = row_dot(r->J, r->MJ);
     r->dinv = den > 2.2204460492503131e-16 ? 1.0 / den : 0.0;
@@ -741,18 +973,29 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
             v1[a] = env->qd[a] + dt * s;
         }
     }
-    double cube_I = 0.0, inv_I = 0.0, inv_m = 0.0;
-    if (cfg->has_cube) {
-        double l = 2.0 * cfg->cube_half;
-        cube_I = cfg->cube_mass / 12.0 * (l * l + l * l);
-        inv_I = 1.0 / cube_I;
-        inv_m = 1.0 / cfg->cube_mass;
-        double cl = PM_LINEAR_DAMPING + PM_LINEAR_DAMPING * v3_norm(env->cvel);
-        double ca = PM_ANGULAR_DAMPING + PM_ANGULAR_DAMPING * v3_norm(env->comg);
+    /* objects: gravity + btMultiBody base damping (k1 + k2 |v| on the linear,
+     * the same on the angular velocity through the inertia, so the angular
+     * deceleration is inertia-free) + the gyroscopic torque -w x (I w),
+     * which vanishes for the isotropic cubes */
+    oobj ob[PO_MAX_OBJECTS];
+    for (int i = 0; i < cfg->n_objects; i++) {
+        const po_body *b = &env->obj[i];
+        object_setup(cfg, env, i, &ob[i]);
+        int o = OBJ_DOF(i);
+        double cl = PM_LINEAR_DAMPING + PM_LINEAR_DAMPING * v3_norm(b->vel);
+        double ca = PM_ANGULAR_DAMPING + PM_ANGULAR_DAMPING * v3_norm(b->omg);
+        double gyro[3] = {0.0, 0.0, 0.0};
+        if (!ob[i].iso) {
+            double Iw[9], Iww[3], t[3];
+            inertia_world(ob[i].R, ob[i].I, Iw);
+            m3_vec(Iw, b->omg, Iww);
+            v3_cross(b->omg, Iww, t);
+            m3_vec(ob[i].Iinv, t, gyro);
+        }
         for (int d = 0; d < 3; d++) {
             double g = d == 2 ? PM_GRAVITY_Z : 0.0;
-            v1[12 + d] = env->cvel[d] + dt * (g - cl * env->cvel[d]);
-            v1[9 + d] = env->comg[d] + dt * (-ca * env->comg[d]);
+            v1[o + 3 + d] = b->vel[d] + dt * (g - cl * b->vel[d]);
+            v1[o + d] = b->omg[d] + dt * (-ca * b->omg[d] - gyro[d]);
         }
     }
 
@@ -773,7 +1016,7 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
                 orow *r = &rows[nr++];
                 memset(r, 0, sizeof *r);
                 r->J[d] = side ? -1.0 : 1.0;
-                finish_row(r, Minv, inv_I, inv_m, v1);
+                finish_row(r, Minv, ob, cfg->n_objects, v1);
                 double rel = row_dot(r->J, v1);
                 double velerr = -rel, poserr = 0.0;
                 int combined = pen > PM_SPLIT_PENETRATION_THRESHOLD;
@@ -791,7 +1034,7 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
             orow *r = &rows[nr++];
             memset(r, 0, sizeof *r);
             r->J[d] = 1.0;
-            finish_row(r, Minv, inv_I, inv_m, v1);
+            finish_row(r, Minv, ob, cfg->n_objects, v1);
             double cur = v1[d];
             double target = env->m_kp[d] * (env->m_target[d] - env->q[d]) / dt + cur +
                             env->m_kd[d] * (env->m_vel[d] - cur);
@@ -804,13 +1047,13 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
     n_noncontact = nr;
 
     ocontact cts[MAX_CONTACTS];
-    int nc = gen_contacts(cfg, env, &k, cts);
+    int nc = gen_contacts(cfg, env, &k, ob, cts);
     int normal_base = nr;
     for (int c = 0; c < nc; c++) {
         orow *r = &rows[nr++];
         memset(r, 0, sizeof *r);
         contact_row_jac(&k, env, &cts[c], cts[c].n, r->J);
-        finish_row(r, Minv, inv_I, inv_m, v1);
+        finish_row(r, Minv, ob, cfg->n_objects, v1);
         double rel = row_dot(r->J, v1);
         double pen = cts[c].dist + PM_LINEAR_SLOP;
         double velerr = -rel, poserr = 0.0;
@@ -830,7 +1073,7 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
             orow *r = &rows[nr++];
             memset(r, 0, sizeof *r);
             contact_row_jac(&k, env, &cts[c], f ? t2 : t1, r->J);
-            finish_row(r, Minv, inv_I, inv_m, v1);
+            finish_row(r, Minv, ob, cfg->n_objects, v1);
             r->rhs = -row_dot(r->J, v1) * r->dinv;
             r->mu = cts[c].mu;
             r->normal = normal_base + c;
@@ -871,20 +1114,22 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
             env->qd[d] = v1[d] + dv[d];
             env->q[d] += dt * env->qd[d] + split_dq[d];
         }
-    if (cfg->has_cube) {
+    for (int i = 0; i < cfg->n_objects; i++) {
+        po_body *b = &env->obj[i];
+        int o = OBJ_DOF(i);
         for (int d = 0; d < 3; d++) {
-            env->comg[d] = v1[9 + d] + dv[9 + d];
-            env->cvel[d] = v1[12 + d] + dv[12 + d];
-            env->cpos[d] += dt * env->cvel[d];
+            b->omg[d] = v1[o + d] + dv[o + d];
+            b->vel[d] = v1[o + 3 + d] + dv[o + 3 + d];
+            b->pos[d] += dt * b->vel[d];
         }
-        double ang = v3_norm(env->comg), ax[3];
+        double ang = v3_norm(b->omg), ax[3];
         if (ang * dt > 0.5 * 1.5707963267948966) ang = 0.5 * 1.5707963267948966 / dt;
         double f = ang < 0.001 ? (0.5 * dt - (dt * dt * dt) * 0.020833333333 * ang * ang) : sin(0.5 * ang * dt) / ang;
-        for (int d = 0; d < 3; d++) ax[d] = env->comg[d] * f;
+        for (int d = 0; d < 3; d++) ax[d] = b->omg[d] * f;
         double dq[4] = {ax[0], ax[1], ax[2], cos(0.5 * ang * dt)}, nq[4];
-        quat_mul(dq, env->cquat, nq);
+        quat_mul(dq, b->quat, nq);
         double nn = sqrt(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
-        for (int d = 0; d < 4; d++) env->cquat[d] = nq[d] / nn;
+        for (int d = 0; d < 4; d++) b->quat[d] = nq[d] / nn;
     }
 }
 
@@ -1007,26 +1252,70 @@ static double uniform(uint64_t rng[4], double lo, double hi) {
 }
 
 /* ------------------------------------------------------------- env layer */
+/* Flip's goal: scipy Rotation.random() (flip.py:70-72) draws from numpy's
+ * unseeded global RandomState, so no seed of the reference reproduces it.
+ * Here it comes from a per-env splitmix64 stream (seeded with the env seed,
+ * separate from np_random so the object draws stay the reference's):
+ * four Box-Muller normals, normalised -- the same uniform distribution over
+ * rotations as R.random(). */
+static uint64_t splitmix64(uint64_t *st) {
+    uint64_t z = (*st += 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+static uint64_t aux_seed(uint64_t seed) { return seed ^ 0x5851F42D4C957F2DULL; }
+
+void po_flip_goal(uint64_t *aux_state, double quat[4]) {
+    double nrm[4];
+    for (int k = 0; k < 2; k++) {
+        double u1 = (double)(splitmix64(aux_state) >> 11) * (1.0 / 9007199254740992.0);
+        double u2 = (double)(splitmix64(aux_state) >> 11) * (1.0 / 9007199254740992.0);
+        double rad = sqrt(-2.0 * log(1.0 - u1)), th = 2.0 * 3.14159265358979323846 * u2;
+        nrm[2 * k] = rad * cos(th);
+        nrm[2 * k + 1] = rad * sin(th);
+    }
+    double n = sqrt(nrm[0] * nrm[0] + nrm[1] * nrm[1] + nrm[2] * nrm[2] + nrm[3] * nrm[3]);
+    for (int d = 0; d < 4; d++) quat[d] = nrm[d] / n;
+}
+
+/* panda_tasks.py:14-113 wiring + each task's _create_scene */
 void po_default_config(po_config *cfg, int task, int control, int reward) {
     memset(cfg, 0, sizeof *cfg);
     cfg->task = task;
     cfg->control = control;
     cfg->reward = reward;
-    /* panda_tasks.py:46,62,78: Reach/Push block the gripper, PickAndPlace not */
-    cfg->block_gripper = task != PO_TASK_PICK_AND_PLACE;
+    /* Reach/Push/Slide block the gripper (panda_tasks.py:62,78,94) */
+    cfg->block_gripper = task == PO_TASK_REACH || task == PO_TASK_PUSH || task == PO_TASK_SLIDE;
     cfg->has_table = cfg->has_plane = 1;
-    cfg->has_cube = task != PO_TASK_REACH;
     cfg->has_robot = 1;
+    cfg->n_objects = task == PO_TASK_REACH ? 0 : (task == PO_TASK_STACK ? 2 : 1);
+    cfg->object_shape = task == PO_TASK_SLIDE ? PO_SHAPE_CYLINDER : PO_SHAPE_BOX;
     cfg->base[0] = PM_BASE_X;
-    cfg->cube_half = PM_CUBE_HALF;
-    cfg->cube_mass = PM_CUBE_MASS;
+    if (task == PO_TASK_SLIDE) {
+        /* create_cylinder(radius = height = object_size / 2) -> half height /2 */
+        cfg->object_half[0] = cfg->object_half[1] = PM_SLIDE_OBJECT_SIZE / 2;
+        cfg->object_half[2] = PM_SLIDE_OBJECT_SIZE / 2 / 2;
+        cfg->object_friction = PM_SLIDE_FRICTION;
+        cfg->table_cx = PM_SLIDE_TABLE_CX;
+        cfg->table_hx = PM_SLIDE_TABLE_HX;
+    } else {
+        cfg->object_half[0] = cfg->object_half[1] = cfg->object_half[2] = PM_OBJECT_SIZE / 2;
+        cfg->object_friction = PM_DEFAULT_FRICTION;
+        cfg->table_cx = PM_TABLE_CX;
+        cfg->table_hx = PM_TABLE_HX;
+    }
+    cfg->table_hy = PM_TABLE_HY;
+    cfg->object_mass = task == PO_TASK_STACK ? PM_STACK_MASS1 : PM_CUBE_MASS;
+    cfg->object2_mass = PM_STACK_MASS2;
 }
 
 void po_init_env(const po_config *cfg, po_env *env) {
     model_init();
     (void)cfg;
     memset(env, 0, sizeof *env);
-    env->cquat[3] = 1.0;
+    for (int i = 0; i < PO_MAX_OBJECTS; i++) env->obj[i].quat[3] = 1.0;
     /* PhysicsServerCommandProcessor::createJointMotors: velocity motor,
      * target 0, kd 1, max impulse 1 on every revolute/prismatic joint */
     for (int d = 0; d < 9; d++) {
@@ -1034,38 +1323,70 @@ void po_init_env(const po_config *cfg, po_env *env) {
         env->m_maximp[d] = PM_DEFAULT_MOTOR_MAX_IMPULSE;
     }
     po_pcg64_seed(0, env->rng);
+    env->rng[4] = aux_seed(0);
 }
 
-int po_obs_dim(const po_config *cfg) {
-    int robot = cfg->block_gripper ? 6 : 7;
-    return robot + (cfg->task == PO_TASK_REACH ? 0 : 12);
+static int task_obs_dim(int task) {
+    switch (task) {
+        case PO_TASK_REACH: return 0;
+        case PO_TASK_STACK: return 24;
+        case PO_TASK_FLIP: return 13;
+        default: return 12;
+    }
 }
+
+int po_obs_dim(const po_config *cfg) { return (cfg->block_gripper ? 6 : 7) + task_obs_dim(cfg->task); }
 
 int po_action_dim(const po_config *cfg) {
     return (cfg->control == PO_CONTROL_EE ? 3 : 7) + (cfg->block_gripper ? 0 : 1);
 }
 
-/* utils.py:4-15 distance + is_success (reach.py:56-58, push.py:89-91):
- * norm of (float32 achieved - float64 goal) in float64, d < 0.05 */
-static double goal_distance(const float ag[3], const double dg[3]) {
-    double d0 = (double)ag[0] - dg[0], d1 = (double)ag[1] - dg[1], d2 = (double)ag[2] - dg[2];
-    double s = d0 * d0;
-    s = s + d1 * d1;
-    s = s + d2 * d2;
+int po_goal_dim(const po_config *cfg) {
+    return cfg->task == PO_TASK_STACK ? 6 : (cfg->task == PO_TASK_FLIP ? 4 : 3);
+}
+
+int po_max_episode_steps(const po_config *cfg) {
+    return cfg->task == PO_TASK_STACK ? PM_STACK_MAX_EPISODE_STEPS : PM_MAX_EPISODE_STEPS;
+}
+
+/* utils.py:4-15 distance: norm of (float32 achieved - float64 goal) in
+ * float64, the squares summed left to right; utils.py:18-30 angle_distance:
+ * 1 - <a, b>^2 (Flip) */
+static double goal_metric(int task, const float *ag, const double *dg) {
+    if (task == PO_TASK_FLIP) {
+        double dot = (double)ag[0] * dg[0];
+        for (int d = 1; d < 4; d++) dot = dot + (double)ag[d] * dg[d];
+        return 1.0 - dot * dot;
+    }
+    int n = task == PO_TASK_STACK ? 6 : 3;
+    double s = 0.0;
+    for (int d = 0; d < n; d++) {
+        double e = (double)ag[d] - dg[d];
+        s = d == 0 ? e * e : s + e * e;
+    }
     return sqrt(s);
 }
 
-uint8_t po_is_success(const float ag[3], const double dg[3]) { return goal_distance(ag, dg) < PM_DISTANCE_THRESHOLD; }
+static double task_threshold(int task) {
+    return task == PO_TASK_STACK ? PM_STACK_DISTANCE_THRESHOLD
+                                 : (task == PO_TASK_FLIP ? PM_FLIP_DISTANCE_THRESHOLD : PM_DISTANCE_THRESHOLD);
+}
 
-/* compute_reward (reach.py:60-65, push.py:93-98, pick_and_place.py:91-96) */
-float po_compute_reward(int reward_type, const float ag[3], const double dg[3]) {
-    double d = goal_distance(ag, dg);
-    if (reward_type == PO_REWARD_SPARSE) return d > PM_DISTANCE_THRESHOLD ? -1.0f : -0.0f;
+/* is_success (reach.py:56-58, push.py:89-91, stack.py:118-121, flip.py:80-82) */
+uint8_t po_is_success(int task, const float *ag, const double *dg) {
+    return goal_metric(task, ag, dg) < task_threshold(task);
+}
+
+/* compute_reward (reach.py:60-65, push.py:93-98, stack.py:123-131, flip.py:84-91) */
+float po_compute_reward(int task, int reward_type, const float *ag, const double *dg) {
+    double d = goal_metric(task, ag, dg);
+    if (reward_type == PO_REWARD_SPARSE) return d > task_threshold(task) ? -1.0f : -0.0f;
     return -(float)d;
 }
 
 /* RobotTaskEnv._get_obs (core.py:229-238) with Panda.get_obs (panda.py:109-119)
- * and Push/PickAndPlace.get_obs (push.py:49-63) */
+ * and the task's get_obs / get_achieved_goal (push.py:49-67, stack.py:65-101,
+ * flip.py:53-64: quaternion instead of Euler angles) */
 void po_get_obs(const po_config *cfg, const po_env *env, float *obs, float *ag, float *dg) {
     double p[3], qq[4], v[3], w[3];
     po_link_state(cfg, env, PM_EE_LINK, p, qq, v, w);
@@ -1073,48 +1394,107 @@ void po_get_obs(const po_config *cfg, const po_env *env, float *obs, float *ag, 
     for (int d = 0; d < 3; d++) obs[o++] = (float)p[d];
     for (int d = 0; d < 3; d++) obs[o++] = (float)v[d];
     if (!cfg->block_gripper) obs[o++] = (float)(env->q[7] + env->q[8]);
-    if (cfg->task != PO_TASK_REACH) {
-        double e[3];
-        po_euler_from_quaternion(env->cquat, e);
-        for (int d = 0; d < 3; d++) obs[o++] = (float)env->cpos[d];
-        for (int d = 0; d < 3; d++) obs[o++] = (float)e[d];
-        for (int d = 0; d < 3; d++) obs[o++] = (float)env->cvel[d];
-        for (int d = 0; d < 3; d++) obs[o++] = (float)env->comg[d];
-        for (int d = 0; d < 3; d++) ag[d] = (float)env->cpos[d];
-    } else {
-        for (int d = 0; d < 3; d++) ag[d] = (float)p[d];
+    for (int i = 0; i < cfg->n_objects; i++) {
+        const po_body *b = &env->obj[i];
+        for (int d = 0; d < 3; d++) obs[o++] = (float)b->pos[d];
+        if (cfg->task == PO_TASK_FLIP) {
+            for (int d = 0; d < 4; d++) obs[o++] = (float)b->quat[d];
+        } else {
+            double e[3];
+            po_euler_from_quaternion(b->quat, e);
+            for (int d = 0; d < 3; d++) obs[o++] = (float)e[d];
+        }
+        for (int d = 0; d < 3; d++) obs[o++] = (float)b->vel[d];
+        for (int d = 0; d < 3; d++) obs[o++] = (float)b->omg[d];
     }
-    for (int d = 0; d < 3; d++) dg[d] = (float)env->goal[d];
+    switch (cfg->task) {
+        case PO_TASK_REACH:
+            for (int d = 0; d < 3; d++) ag[d] = (float)p[d];
+            break;
+        case PO_TASK_FLIP:
+            for (int d = 0; d < 4; d++) ag[d] = (float)env->obj[0].quat[d];
+            break;
+        case PO_TASK_STACK:
+            for (int d = 0; d < 3; d++) {
+                ag[d] = (float)env->obj[0].pos[d];
+                ag[3 + d] = (float)env->obj[1].pos[d];
+            }
+            break;
+        default:
+            for (int d = 0; d < 3; d++) ag[d] = (float)env->obj[0].pos[d];
+    }
+    int gd = po_goal_dim(cfg);
+    for (int d = 0; d < gd; d++) dg[d] = (float)env->goal[d];
+}
+
+static void place_object(po_body *b, const double pos[3], const double quat[4]) {
+    memcpy(b->pos, pos, sizeof(double) * 3);
+    memcpy(b->quat, quat, sizeof(double) * 4);
 }
 
 /* RobotTaskEnv.reset (core.py:240-250): new Generator(PCG64(SeedSequence(seed)))
  * when a seed is given; Panda.reset -> neutral joints with zero velocity
- * (panda.py:121-126); Task.reset draws the goal then the object
- * (reach.py:47-54, push.py:69-87, pick_and_place.py:65-85).  The object's
- * velocity is not reset (only resetBasePositionAndOrientation is called). */
+ * (panda.py:121-126); Task.reset draws the goal then the object(s) in the
+ * reference's order (reach.py:47-54, push.py:69-87, pick_and_place.py:65-85,
+ * slide.py:69-87, stack.py:103-116, flip.py:66-78).  Object velocities are
+ * not reset (only resetBasePositionAndOrientation is called). */
 void po_reset(const po_config *cfg, po_env *env, int has_seed, uint64_t seed, float *obs, float *ag, float *dg) {
     model_init();
-    if (has_seed) po_pcg64_seed(seed, env->rng);
+    if (has_seed) {
+        po_pcg64_seed(seed, env->rng);
+        env->rng[4] = aux_seed(seed);
+    }
     static const double neutral[9] = PM_NEUTRAL_Q;
+    static const double ident[4] = {0.0, 0.0, 0.0, 1.0};
     for (int d = 0; d < 9; d++) { env->q[d] = neutral[d]; env->qd[d] = 0.0; }
-    if (cfg->task == PO_TASK_REACH) {
-        env->goal[0] = uniform(env->rng, -0.15, 0.15);
-        env->goal[1] = uniform(env->rng, -0.15, 0.15);
-        env->goal[2] = uniform(env->rng, 0.0, 0.3);
-    } else {
-        double zr = cfg->task == PO_TASK_PICK_AND_PLACE ? 0.2 : 0.0;
-        double n0 = uniform(env->rng, -0.15, 0.15), n1 = uniform(env->rng, -0.15, 0.15), n2 = uniform(env->rng, 0.0, zr);
-        if (cfg->task == PO_TASK_PICK_AND_PLACE && po_pcg64_double(env->rng) < 0.3) n2 = 0.0;
-        /* object_size / 2 of the task (push.py:19), not the physics shape */
-        env->goal[0] = 0.0 + n0;
-        env->goal[1] = 0.0 + n1;
-        env->goal[2] = PM_CUBE_HALF + n2;
-        double o0 = uniform(env->rng, -0.15, 0.15), o1 = uniform(env->rng, -0.15, 0.15), o2 = uniform(env->rng, 0.0, 0.0);
-        env->cpos[0] = 0.0 + o0;
-        env->cpos[1] = 0.0 + o1;
-        env->cpos[2] = PM_CUBE_HALF + o2;
-        env->cquat[0] = env->cquat[1] = env->cquat[2] = 0.0;
-        env->cquat[3] = 1.0;
+    uint64_t *r = env->rng;
+    const double xy = 0.3 / 2; /* goal_xy_range / 2 = obj_xy_range / 2 */
+    switch (cfg->task) {
+        case PO_TASK_REACH:
+            env->goal[0] = uniform(r, -0.3 / 2, 0.3 / 2);
+            env->goal[1] = uniform(r, -0.3 / 2, 0.3 / 2);
+            env->goal[2] = uniform(r, 0.0, 0.3);
+            break;
+        case PO_TASK_PUSH:
+        case PO_TASK_PICK_AND_PLACE:
+        case PO_TASK_SLIDE: {
+            double size = cfg->task == PO_TASK_SLIDE ? PM_SLIDE_OBJECT_SIZE : PM_OBJECT_SIZE;
+            double gx = cfg->task == PO_TASK_SLIDE ? PM_SLIDE_GOAL_X_OFFSET : 0.0;
+            double zr = cfg->task == PO_TASK_PICK_AND_PLACE ? 0.2 : 0.0;
+            double n0 = uniform(r, -xy + gx, xy + gx), n1 = uniform(r, -xy, xy), n2 = uniform(r, 0.0, zr);
+            if (cfg->task == PO_TASK_PICK_AND_PLACE && po_pcg64_double(r) < 0.3) n2 = 0.0;
+            env->goal[0] = 0.0 + n0;
+            env->goal[1] = 0.0 + n1;
+            env->goal[2] = size / 2 + n2;
+            double o0 = uniform(r, -xy, xy), o1 = uniform(r, -xy, xy), o2 = uniform(r, 0.0, 0.0);
+            double pos[3] = {0.0 + o0, 0.0 + o1, size / 2 + o2};
+            place_object(&env->obj[0], pos, ident);
+            break;
+        }
+        case PO_TASK_STACK: {
+            double size = PM_OBJECT_SIZE;
+            double n0 = uniform(r, -xy, xy), n1 = uniform(r, -xy, xy), n2 = uniform(r, 0.0, 0.0);
+            env->goal[0] = 0.0 + n0;
+            env->goal[1] = 0.0 + n1;
+            env->goal[2] = size / 2 + n2;
+            env->goal[3] = 0.0 + n0;
+            env->goal[4] = 0.0 + n1;
+            env->goal[5] = 3 * size / 2 + n2;
+            double a0 = uniform(r, -xy, xy), a1 = uniform(r, -xy, xy), a2 = uniform(r, 0.0, 0.0);
+            double b0 = uniform(r, -xy, xy), b1 = uniform(r, -xy, xy), b2 = uniform(r, 0.0, 0.0);
+            double p1[3] = {0.0 + a0, 0.0 + a1, size / 2 + a2}, p2[3] = {0.0 + b0, 0.0 + b1, 3 * size / 2 + b2};
+            place_object(&env->obj[0], p1, ident);
+            place_object(&env->obj[1], p2, ident);
+            break;
+        }
+        case PO_TASK_FLIP: {
+            po_flip_goal(&env->rng[4], env->goal);
+            double o0 = uniform(r, -xy, xy), o1 = uniform(r, -xy, xy), o2 = uniform(r, 0.0, 0.0);
+            double pos[3] = {0.0 + o0, 0.0 + o1, PM_OBJECT_SIZE / 2 + o2};
+            /* set_base_pose with Euler zeros -> getQuaternionFromEuler = identity */
+            place_object(&env->obj[0], pos, ident);
+            break;
+        }
     }
     env->elapsed = 0;
     if (obs) po_get_obs(cfg, env, obs, ag, dg);
@@ -1147,7 +1527,7 @@ static void set_action(const po_config *cfg, po_env *env, const float *action) {
     po_control_joints(env, 9, joints, target, forces);
 }
 
-/* RobotTaskEnv.step (core.py:280-289) + TimeLimit(50) (__init__.py:18-40) */
+/* RobotTaskEnv.step (core.py:280-289) + TimeLimit (__init__.py:18-46) */
 void po_step(const po_config *cfg, po_env *env, const float *action, float *obs, float *ag, float *dg,
              float *reward, uint8_t *terminated, uint8_t *truncated, int autoreset, float *final_obs,
              float *final_ag, po_stats *stats) {
@@ -1155,14 +1535,14 @@ void po_step(const po_config *cfg, po_env *env, const float *action, float *obs,
     set_action(cfg, env, action);
     po_sim_step(cfg, env, stats);
     po_get_obs(cfg, env, obs, ag, dg);
-    *terminated = po_is_success(ag, env->goal);
-    *reward = po_compute_reward(cfg->reward, ag, env->goal);
+    *terminated = po_is_success(cfg->task, ag, env->goal);
+    *reward = po_compute_reward(cfg->task, cfg->reward, ag, env->goal);
     env->elapsed += 1;
-    *truncated = env->elapsed >= PM_MAX_EPISODE_STEPS;
+    *truncated = env->elapsed >= po_max_episode_steps(cfg);
     if (autoreset && (*terminated || *truncated)) {
-        int od = po_obs_dim(cfg);
+        int od = po_obs_dim(cfg), gd = po_goal_dim(cfg);
         if (final_obs) memcpy(final_obs, obs, sizeof(float) * od);
-        if (final_ag) memcpy(final_ag, ag, sizeof(float) * 3);
+        if (final_ag) memcpy(final_ag, ag, sizeof(float) * gd);
         po_reset(cfg, env, 0, 0, obs, ag, dg);
     }
 }
@@ -1170,8 +1550,8 @@ void po_step(const po_config *cfg, po_env *env, const float *action, float *obs,
 void po_step_batch(const po_config *cfg, po_env *envs, int n, const float *actions, float *obs, float *ag,
                    float *dg, float *reward, uint8_t *terminated, uint8_t *truncated, int autoreset,
                    po_stats *stats) {
-    int na = po_action_dim(cfg), od = po_obs_dim(cfg);
+    int na = po_action_dim(cfg), od = po_obs_dim(cfg), gd = po_goal_dim(cfg);
     for (int i = 0; i < n; i++)
-        po_step(cfg, &envs[i], actions + (size_t)i * na, obs + (size_t)i * od, ag + (size_t)i * 3,
-                dg + (size_t)i * 3, reward + i, terminated + i, truncated + i, autoreset, NULL, NULL, stats);
+        po_step(cfg, &envs[i], actions + (size_t)i * na, obs + (size_t)i * od, ag + (size_t)i * gd,
+                dg + (size_t)i * gd, reward + i, terminated + i, truncated + i, autoreset, NULL, NULL, stats);
 }

@@ -26,24 +26,43 @@
 extern "C" {
 #endif
 
-enum { PO_TASK_REACH = 0, PO_TASK_PUSH = 1, PO_TASK_PICK_AND_PLACE = 2 };
+enum {
+    PO_TASK_REACH = 0,
+    PO_TASK_PUSH = 1,
+    PO_TASK_PICK_AND_PLACE = 2,
+    PO_TASK_SLIDE = 3,
+    PO_TASK_STACK = 4,
+    PO_TASK_FLIP = 5
+};
 enum { PO_CONTROL_EE = 0, PO_CONTROL_JOINTS = 1 };
 enum { PO_REWARD_SPARSE = 0, PO_REWARD_DENSE = 1 };
+enum { PO_SHAPE_BOX = 0, PO_SHAPE_CYLINDER = 1 };
+#define PO_MAX_OBJECTS 2
+#define PO_MAX_GOAL 6
 
+/* mirrors ps_config (include/pandasim.h) in fp64, plus has_robot for the
+ * engine-level KAT scenes that have no robot */
 typedef struct {
     int32_t task, control, reward, block_gripper;
-    int32_t has_table, has_plane, has_cube, has_robot;
+    int32_t has_table, has_plane, n_objects, object_shape;
+    int32_t has_robot, reserved;
     double base[3];
-    double cube_half, cube_mass;
+    double object_half[3];
+    double object_mass, object2_mass, object_friction;
+    double table_cx, table_hx, table_hy;
 } po_config;
+
+typedef struct {
+    double pos[3], quat[4], vel[3], omg[3]; /* quat (x,y,z,w) body->world */
+} po_body;
 
 typedef struct {
     double q[9], qd[9];
     double m_target[9], m_kp[9], m_kd[9], m_vel[9], m_maximp[9];
-    double cpos[3], cquat[4], cvel[3], comg[3]; /* cube: quat (x,y,z,w) base->world */
-    double goal[3];
+    po_body obj[PO_MAX_OBJECTS];
+    double goal[PO_MAX_GOAL];
     int64_t elapsed;
-    uint64_t rng[4]; /* PCG64 state hi, lo, inc hi, lo */
+    uint64_t rng[5]; /* PCG64 state hi, lo, inc hi, lo; splitmix64 state of Flip's goal stream */
 } po_env;
 
 typedef struct {
@@ -66,6 +85,8 @@ void po_euler_from_quaternion(const double q[4], double rpy[3]);
 /* --- env-level (core.py) --- */
 int po_obs_dim(const po_config *cfg);
 int po_action_dim(const po_config *cfg);
+int po_goal_dim(const po_config *cfg);
+int po_max_episode_steps(const po_config *cfg);
 void po_reset(const po_config *cfg, po_env *env, int has_seed, uint64_t seed, float *obs, float *ag, float *dg);
 void po_get_obs(const po_config *cfg, const po_env *env, float *obs, float *ag, float *dg);
 void po_step(const po_config *cfg, po_env *env, const float *action, float *obs, float *ag, float *dg,
@@ -74,10 +95,13 @@ void po_step(const po_config *cfg, po_env *env, const float *action, float *obs,
 void po_step_batch(const po_config *cfg, po_env *envs, int n, const float *actions, float *obs, float *ag,
                    float *dg, float *reward, uint8_t *terminated, uint8_t *truncated, int autoreset,
                    po_stats *stats);
-float po_compute_reward(int reward_type, const float ag[3], const double dg[3]);
-uint8_t po_is_success(const float ag[3], const double dg[3]);
+/* Task.compute_reward / is_success of one (float32 achieved, float64 desired)
+ * goal pair of `task` (goal_dim values each) */
+float po_compute_reward(int task, int reward_type, const float *ag, const double *dg);
+uint8_t po_is_success(int task, const float *ag, const double *dg);
 
-/* --- numpy SeedSequence / PCG64 --- */
+/* --- numpy SeedSequence / PCG64; splitmix64 + Box-Muller for Flip's goal --- */
+void po_flip_goal(uint64_t *aux_state, double quat[4]);
 void po_pcg64_seed(uint64_t seed, uint64_t rng[4]);
 uint64_t po_pcg64_next(uint64_t rng[4]);
 double po_pcg64_double(uint64_t rng[4]);

@@ -22,12 +22,13 @@ struct ps_ctx {
 };
 
 #ifdef PS_PROFILE_PHASES
-__device__ unsigned long long ps_phase_cycles[PS_NUM_PHASES];
+__device__ unsigned long long ps_phase_cycles[PS_NUM_PROF_SLOTS];
 extern "C" int ps_debug_phase_cycles(unsigned long long *out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ps_phase_cycles), sizeof(unsigned long long) * PS_NUM_PHASES) != hipSuccess)
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(ps_phase_cycles), sizeof(unsigned long long) * PS_NUM_PROF_SLOTS) !=
+        hipSuccess)
         return PS_ERR_HIP;
     if (reset) {
-        unsigned long long z[PS_NUM_PHASES] = {0};
+        unsigned long long z[PS_NUM_PROF_SLOTS] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(ps_phase_cycles), z, sizeof z) != hipSuccess) return PS_ERR_HIP;
     }
     return PS_OK;
@@ -38,13 +39,33 @@ namespace {
 
 constexpr int kBlock = 64;
 
+// Per-task constants (panda_gym/__init__.py:8-54, envs/panda_tasks.py:14-113,
+// tasks/*.py): objects, shape, goal size, TimeLimit and success threshold.
+template <int TASK>
+struct TaskTraits {
+    static constexpr int NOBJ = TASK == PS_TASK_REACH ? 0 : (TASK == PS_TASK_STACK ? 2 : 1);
+    static constexpr int SHAPE = TASK == PS_TASK_SLIDE ? PS_SHAPE_CYLINDER : PS_SHAPE_BOX;
+    static constexpr int GOAL = TASK == PS_TASK_STACK ? 6 : (TASK == PS_TASK_FLIP ? 4 : 3);
+    static constexpr int STEPS = TASK == PS_TASK_STACK ? PM_STACK_MAX_EPISODE_STEPS : PM_MAX_EPISODE_STEPS;
+    static constexpr double THRESHOLD = TASK == PS_TASK_STACK ? PM_STACK_DISTANCE_THRESHOLD
+                                        : TASK == PS_TASK_FLIP ? PM_FLIP_DISTANCE_THRESHOLD
+                                                               : PM_DISTANCE_THRESHOLD;
+};
+
+int task_nobj(int task) { return task == PS_TASK_REACH ? 0 : (task == PS_TASK_STACK ? 2 : 1); }
+int task_goal_dim(int task) { return task == PS_TASK_STACK ? 6 : (task == PS_TASK_FLIP ? 4 : 3); }
+int task_obs_dim(int task) {
+    return task == PS_TASK_REACH ? 0 : (task == PS_TASK_STACK ? 24 : (task == PS_TASK_FLIP ? 13 : 12));
+}
+
 struct StateView {
-    float *f;  // [76][stride]
+    float *f;  // [PS_NUM_FLOAT_ROWS][stride]
     double *goal;
     uint64_t *rng;
     int32_t *elapsed;
     int64_t stride;
     PS_D float &F(int row, int64_t i) const { return f[row * stride + i]; }
+    PS_D double &G(int k, int64_t i) const { return goal[k * stride + i]; }
 };
 
 StateView view_of(const ps_ctx *c, void *state) {
@@ -68,11 +89,15 @@ struct KParams {
 Scene scene_of(const ps_config &c) {
     Scene s;
     s.base = mk(c.base[0], c.base[1], c.base[2]);
-    s.half = c.cube_half;
-    s.mass = c.cube_mass;
+    s.half = mk(c.object_half[0], c.object_half[1], c.object_half[2]);
+    s.mass = c.object_mass;
+    s.mass2 = c.object2_mass;
+    s.fric = c.object_friction;
+    s.table_cx = c.table_cx;
+    s.table_hx = c.table_hx;
+    s.table_hy = c.table_hy;
     s.has_table = c.has_table;
     s.has_plane = c.has_plane;
-    s.has_cube = c.has_cube;
     return s;
 }
 
@@ -111,13 +136,35 @@ PS_D void store_motors(const StateView &s, int64_t i, const Motors &m) {
         s.F(PS_F_MIMP + d, i) = m.imp[d];
     }
 }
+PS_D int body_row(int b) { return b == 0 ? PS_F_CPOS : PS_F_C2POS; }
+PS_D void load_body(const StateView &s, int64_t i, int b, Body &c) {
+    int r = body_row(b);
+    c.pos = mk(s.F(r, i), s.F(r + 1, i), s.F(r + 2, i));
+    c.quat = Q4{s.F(r + 3, i), s.F(r + 4, i), s.F(r + 5, i), s.F(r + 6, i)};
+    c.vel = mk(s.F(r + 7, i), s.F(r + 8, i), s.F(r + 9, i));
+    c.omg = mk(s.F(r + 10, i), s.F(r + 11, i), s.F(r + 12, i));
+}
+PS_D void store_body(const StateView &s, int64_t i, int b, const Body &c) {
+    int r = body_row(b);
+    s.F(r, i) = c.pos.x; s.F(r + 1, i) = c.pos.y; s.F(r + 2, i) = c.pos.z;
+    s.F(r + 3, i) = c.quat.x; s.F(r + 4, i) = c.quat.y; s.F(r + 5, i) = c.quat.z; s.F(r + 6, i) = c.quat.w;
+    s.F(r + 7, i) = c.vel.x; s.F(r + 8, i) = c.vel.y; s.F(r + 9, i) = c.vel.z;
+    s.F(r + 10, i) = c.omg.x; s.F(r + 11, i) = c.omg.y; s.F(r + 12, i) = c.omg.z;
+}
+PS_D Pcg load_rng(const StateView &s, int64_t i) {
+    return Pcg{s.rng[i], s.rng[s.stride + i], s.rng[2 * s.stride + i], s.rng[3 * s.stride + i]};
+}
+PS_D void store_rng(const StateView &s, int64_t i, const Pcg &r) {
+    s.rng[i] = r.sh; s.rng[s.stride + i] = r.sl; s.rng[2 * s.stride + i] = r.ih; s.rng[3 * s.stride + i] = r.il;
+}
+PS_D uint64_t &aux_rng(const StateView &s, int64_t i) { return s.rng[4 * s.stride + i]; }
 
 // The motor rows' targets/gains are constant over a control step: they are
 // re-read from the (L2-resident) state buffer at every substep instead of
 // occupying 45 registers through the solver.  The index goes through an empty
 // asm so the loads cannot be hoisted out of the substep loop.
-template <bool HAS_CUBE, bool STD_MOTORS>
-PS_D void run_substeps(const KParams &P, int64_t i, int n, float q[9], float qd[9], Cube &cb,
+template <int NOBJ, int SHAPE, bool STD_MOTORS>
+PS_D void run_substeps(const KParams &P, int64_t i, int n, float q[9], float qd[9], Body *bd,
                        const MJStore &lds PS_PROF_PARAM) {
     for (int st = 0; st < n; st++) {
         int64_t ii = i;
@@ -129,27 +176,8 @@ PS_D void run_substeps(const KParams &P, int64_t i, int n, float q[9], float qd[
         } else {
             load_motors(P.s, ii, m);
         }
-        substep<HAS_CUBE, STD_MOTORS>(P.sc, q, qd, m, cb, lds PS_PROF_ARG);
+        substep<NOBJ, SHAPE, STD_MOTORS>(P.sc, q, qd, m, bd, lds PS_PROF_ARG);
     }
-}
-PS_D void load_cube(const StateView &s, int64_t i, Cube &c) {
-    c.pos = mk(s.F(PS_F_CPOS, i), s.F(PS_F_CPOS + 1, i), s.F(PS_F_CPOS + 2, i));
-    c.quat = Q4{s.F(PS_F_CQUAT, i), s.F(PS_F_CQUAT + 1, i), s.F(PS_F_CQUAT + 2, i), s.F(PS_F_CQUAT + 3, i)};
-    c.vel = mk(s.F(PS_F_CVEL, i), s.F(PS_F_CVEL + 1, i), s.F(PS_F_CVEL + 2, i));
-    c.omg = mk(s.F(PS_F_COMG, i), s.F(PS_F_COMG + 1, i), s.F(PS_F_COMG + 2, i));
-}
-PS_D void store_cube(const StateView &s, int64_t i, const Cube &c) {
-    s.F(PS_F_CPOS, i) = c.pos.x; s.F(PS_F_CPOS + 1, i) = c.pos.y; s.F(PS_F_CPOS + 2, i) = c.pos.z;
-    s.F(PS_F_CQUAT, i) = c.quat.x; s.F(PS_F_CQUAT + 1, i) = c.quat.y;
-    s.F(PS_F_CQUAT + 2, i) = c.quat.z; s.F(PS_F_CQUAT + 3, i) = c.quat.w;
-    s.F(PS_F_CVEL, i) = c.vel.x; s.F(PS_F_CVEL + 1, i) = c.vel.y; s.F(PS_F_CVEL + 2, i) = c.vel.z;
-    s.F(PS_F_COMG, i) = c.omg.x; s.F(PS_F_COMG + 1, i) = c.omg.y; s.F(PS_F_COMG + 2, i) = c.omg.z;
-}
-PS_D Pcg load_rng(const StateView &s, int64_t i) {
-    return Pcg{s.rng[i], s.rng[s.stride + i], s.rng[2 * s.stride + i], s.rng[3 * s.stride + i]};
-}
-PS_D void store_rng(const StateView &s, int64_t i, const Pcg &r) {
-    s.rng[i] = r.sh; s.rng[s.stride + i] = r.sl; s.rng[2 * s.stride + i] = r.ih; s.rng[3 * s.stride + i] = r.il;
 }
 
 // ------------------------------------------------------- task layer pieces
@@ -165,63 +193,178 @@ PS_D void ee_state(const Scene &sc, const float q[9], const float qd[9], V3 &pos
     vel = v;
 }
 
-// RobotTaskEnv._get_obs (core.py:229-238)
+// RobotTaskEnv._get_obs (core.py:229-238): robot obs (panda.py:109-119), the
+// task obs (push.py:49-63; stack.py:65-91 both objects; flip.py:53-60 with the
+// quaternion in place of Euler angles) and the achieved goal
 template <int TASK>
-PS_D void write_obs(const KParams &P, int64_t i, const float q[9], const float qd[9], const Cube &cb,
-                    const double g[3], float *obs, float *ag, float *dg) {
+PS_D void write_obs(const KParams &P, int64_t i, const float q[9], const float qd[9], const Body *bd,
+                    const double g[6], float *obs, float *ag, float *dg) {
+    using T = TaskTraits<TASK>;
     V3 p, v;
     ee_state(P.sc, q, qd, p, v);
-    float o[19];
+    float o[31];
     o[0] = p.x; o[1] = p.y; o[2] = p.z;
     o[3] = v.x; o[4] = v.y; o[5] = v.z;
     int k = 6;
     if (!P.block_gripper) o[k++] = q[7] + q[8];
-    float a0 = p.x, a1 = p.y, a2 = p.z;
-    if constexpr (TASK != PS_TASK_REACH) {
-        V3 e = euler_from_quat(cb.quat);
+#pragma unroll
+    for (int b = 0; b < T::NOBJ; b++) {
+        const Body &cb = bd[b];
         o[k] = cb.pos.x; o[k + 1] = cb.pos.y; o[k + 2] = cb.pos.z;
-        o[k + 3] = e.x; o[k + 4] = e.y; o[k + 5] = e.z;
-        o[k + 6] = cb.vel.x; o[k + 7] = cb.vel.y; o[k + 8] = cb.vel.z;
-        o[k + 9] = cb.omg.x; o[k + 10] = cb.omg.y; o[k + 11] = cb.omg.z;
-        a0 = cb.pos.x; a1 = cb.pos.y; a2 = cb.pos.z;
+        k += 3;
+        if constexpr (TASK == PS_TASK_FLIP) {
+            o[k] = cb.quat.x; o[k + 1] = cb.quat.y; o[k + 2] = cb.quat.z; o[k + 3] = cb.quat.w;
+            k += 4;
+        } else {
+            V3 e = euler_from_quat(cb.quat);
+            o[k] = e.x; o[k + 1] = e.y; o[k + 2] = e.z;
+            k += 3;
+        }
+        o[k] = cb.vel.x; o[k + 1] = cb.vel.y; o[k + 2] = cb.vel.z;
+        o[k + 3] = cb.omg.x; o[k + 4] = cb.omg.y; o[k + 5] = cb.omg.z;
+        k += 6;
+    }
+    float a[6];
+    if constexpr (TASK == PS_TASK_REACH) {
+        a[0] = p.x; a[1] = p.y; a[2] = p.z;
+    } else if constexpr (TASK == PS_TASK_FLIP) {
+        a[0] = bd[0].quat.x; a[1] = bd[0].quat.y; a[2] = bd[0].quat.z; a[3] = bd[0].quat.w;
+    } else {
+        a[0] = bd[0].pos.x; a[1] = bd[0].pos.y; a[2] = bd[0].pos.z;
+        if constexpr (T::NOBJ == 2) { a[3] = bd[1].pos.x; a[4] = bd[1].pos.y; a[5] = bd[1].pos.z; }
     }
     if (obs) {
 #pragma unroll
-        for (int j = 0; j < 19; j++)
+        for (int j = 0; j < 31; j++)
             if (j < P.obs_dim) obs[i * P.obs_dim + j] = o[j];
     }
-    if (ag) { ag[i * 3] = a0; ag[i * 3 + 1] = a1; ag[i * 3 + 2] = a2; }
+    if (ag) {
+#pragma unroll
+        for (int j = 0; j < T::GOAL; j++) ag[i * T::GOAL + j] = a[j];
+    }
     if (dg) {
-        dg[i * 3] = __double2float_rn(g[0]);
-        dg[i * 3 + 1] = __double2float_rn(g[1]);
-        dg[i * 3 + 2] = __double2float_rn(g[2]);
+#pragma unroll
+        for (int j = 0; j < T::GOAL; j++) dg[i * T::GOAL + j] = __double2float_rn(g[j]);
     }
 }
 
-// Panda.reset + Task.reset (core.py:245-247)
+// achieved goal of the stepped state (float32, as _get_obs casts it)
 template <int TASK>
-PS_D void reset_env(const KParams &P, int64_t i, float q[9], float qd[9], Cube &cb, double g[3], Pcg &r) {
+PS_D void achieved(const KParams &P, const float q[9], const float qd[9], const Body *bd, float a[6]) {
+    if constexpr (TASK == PS_TASK_REACH) {
+        V3 p, v;
+        ee_state(P.sc, q, qd, p, v);
+        a[0] = p.x; a[1] = p.y; a[2] = p.z;
+    } else if constexpr (TASK == PS_TASK_FLIP) {
+        a[0] = bd[0].quat.x; a[1] = bd[0].quat.y; a[2] = bd[0].quat.z; a[3] = bd[0].quat.w;
+    } else {
+        a[0] = bd[0].pos.x; a[1] = bd[0].pos.y; a[2] = bd[0].pos.z;
+        if constexpr (TaskTraits<TASK>::NOBJ == 2) { a[3] = bd[1].pos.x; a[4] = bd[1].pos.y; a[5] = bd[1].pos.z; }
+    }
+}
+
+// utils.distance (3 or 6 values) / utils.angle_distance (Flip) of float32
+// achieved vs float64 desired, in float64 as numpy promotes
+template <int TASK>
+PS_D double goal_metric(const float a[6], const double g[6]) {
+#pragma clang fp contract(off)
+    if constexpr (TASK == PS_TASK_FLIP) {
+        double dot = opaque(__dmul_rn((double)a[0], g[0]));
+#pragma unroll
+        for (int k = 1; k < 4; k++) dot = __dadd_rn(dot, opaque(__dmul_rn((double)a[k], g[k])));
+        return __dsub_rn(1.0, opaque(__dmul_rn(dot, dot)));
+    } else {
+        constexpr int N = TaskTraits<TASK>::GOAL;
+        double s = 0.0;
+#pragma unroll
+        for (int k = 0; k < N; k++) {
+            double e = __dsub_rn((double)a[k], g[k]);
+            double e2 = opaque(__dmul_rn(e, e));
+            s = k == 0 ? e2 : __dadd_rn(s, e2);
+        }
+        return __dsqrt_rn(s);
+    }
+}
+
+PS_D float reward_for(int reward_type, double d, double thr) {
+    if (reward_type == 0) return d > thr ? -1.0f : -0.0f;
+    return -__double2float_rn(d);
+}
+
+// splitmix64 stream of Flip's goal (oracle po_flip_goal): R.random() as four
+// Box-Muller normals, normalised (flip.py:70-72)
+PS_D uint64_t splitmix64(uint64_t &st) {
+    uint64_t z = (st += 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+PS_D uint64_t aux_seed(uint64_t seed) { return seed ^ 0x5851F42D4C957F2DULL; }
+PS_D void random_rotation(uint64_t &st, double q[4]) {
+    double nrm[4];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        double u1 = (double)(splitmix64(st) >> 11) * (1.0 / 9007199254740992.0);
+        double u2 = (double)(splitmix64(st) >> 11) * (1.0 / 9007199254740992.0);
+        double rad = sqrt(-2.0 * log(1.0 - u1)), th = 2.0 * 3.14159265358979323846 * u2;
+        nrm[2 * k] = rad * cos(th);
+        nrm[2 * k + 1] = rad * sin(th);
+    }
+    double n = sqrt(nrm[0] * nrm[0] + nrm[1] * nrm[1] + nrm[2] * nrm[2] + nrm[3] * nrm[3]);
+#pragma unroll
+    for (int d = 0; d < 4; d++) q[d] = nrm[d] / n;
+}
+
+PS_D void place(Body &b, double x, double y, double z) {
+    b.pos = mk((float)x, (float)y, (float)z);
+    b.quat = Q4{0.0f, 0.0f, 0.0f, 1.0f};
+    // the velocity is not reset (resetBasePositionAndOrientation only)
+}
+
+// Panda.reset + Task.reset (core.py:245-247): goal then object draws in the
+// reference's order (reach.py:47-54, push.py:69-87, pick_and_place.py:65-85,
+// slide.py:69-87, stack.py:103-116, flip.py:66-78)
+template <int TASK>
+PS_D void reset_env(float q[9], float qd[9], Body *bd, double g[6], Pcg &r, uint64_t &aux) {
 #pragma unroll
     for (int d = 0; d < 9; d++) {
         q[d] = (float)neutral_q(d);
         qd[d] = 0.0f;
     }
+    constexpr double xy = 0.3 / 2;  // goal_xy_range / 2 = obj_xy_range / 2
     if constexpr (TASK == PS_TASK_REACH) {
-        g[0] = uniform(r, -0.15, 0.15);
-        g[1] = uniform(r, -0.15, 0.15);
+        g[0] = uniform(r, -xy, xy);
+        g[1] = uniform(r, -xy, xy);
         g[2] = uniform(r, 0.0, 0.3);
-    } else {
-        const double zr = TASK == PS_TASK_PICK_AND_PLACE ? 0.2 : 0.0;
-        double n0 = uniform(r, -0.15, 0.15), n1 = uniform(r, -0.15, 0.15), n2 = uniform(r, 0.0, zr);
-        if (TASK == PS_TASK_PICK_AND_PLACE && pcg_double(r) < 0.3) n2 = 0.0;
-        const double half = PM_CUBE_HALF;  // object_size / 2 in fp64 (push.py:19, 75-80)
+    } else if constexpr (TASK == PS_TASK_STACK) {
+        constexpr double size = PM_OBJECT_SIZE;
+        double n0 = uniform(r, -xy, xy), n1 = uniform(r, -xy, xy), n2 = uniform(r, 0.0, 0.0);
         g[0] = __dadd_rn(0.0, n0);
         g[1] = __dadd_rn(0.0, n1);
-        g[2] = __dadd_rn(half, n2);
-        double o0 = uniform(r, -0.15, 0.15), o1 = uniform(r, -0.15, 0.15), o2 = uniform(r, 0.0, 0.0);
-        cb.pos = mk((float)__dadd_rn(0.0, o0), (float)__dadd_rn(0.0, o1), (float)__dadd_rn(half, o2));
-        cb.quat = Q4{0.0f, 0.0f, 0.0f, 1.0f};
-        // object velocity is not reset (resetBasePositionAndOrientation only)
+        g[2] = __dadd_rn(size / 2, n2);
+        g[3] = __dadd_rn(0.0, n0);
+        g[4] = __dadd_rn(0.0, n1);
+        g[5] = __dadd_rn(3 * size / 2, n2);
+        double a0 = uniform(r, -xy, xy), a1 = uniform(r, -xy, xy), a2 = uniform(r, 0.0, 0.0);
+        double b0 = uniform(r, -xy, xy), b1 = uniform(r, -xy, xy), b2 = uniform(r, 0.0, 0.0);
+        place(bd[0], __dadd_rn(0.0, a0), __dadd_rn(0.0, a1), __dadd_rn(size / 2, a2));
+        place(bd[1], __dadd_rn(0.0, b0), __dadd_rn(0.0, b1), __dadd_rn(3 * size / 2, b2));
+    } else if constexpr (TASK == PS_TASK_FLIP) {
+        random_rotation(aux, g);
+        double o0 = uniform(r, -xy, xy), o1 = uniform(r, -xy, xy), o2 = uniform(r, 0.0, 0.0);
+        place(bd[0], __dadd_rn(0.0, o0), __dadd_rn(0.0, o1), __dadd_rn(PM_OBJECT_SIZE / 2, o2));
+    } else {
+        // Push, PickAndPlace, Slide
+        constexpr double size = TASK == PS_TASK_SLIDE ? PM_SLIDE_OBJECT_SIZE : PM_OBJECT_SIZE;
+        constexpr double gx = TASK == PS_TASK_SLIDE ? PM_SLIDE_GOAL_X_OFFSET : 0.0;
+        constexpr double zr = TASK == PS_TASK_PICK_AND_PLACE ? 0.2 : 0.0;
+        double n0 = uniform(r, -xy + gx, xy + gx), n1 = uniform(r, -xy, xy), n2 = uniform(r, 0.0, zr);
+        if (TASK == PS_TASK_PICK_AND_PLACE && pcg_double(r) < 0.3) n2 = 0.0;
+        g[0] = __dadd_rn(0.0, n0);
+        g[1] = __dadd_rn(0.0, n1);
+        g[2] = __dadd_rn(size / 2, n2);
+        double o0 = uniform(r, -xy, xy), o1 = uniform(r, -xy, xy), o2 = uniform(r, 0.0, 0.0);
+        place(bd[0], __dadd_rn(0.0, o0), __dadd_rn(0.0, o1), __dadd_rn(size / 2, o2));
     }
 }
 
@@ -241,11 +384,7 @@ PS_D void set_action(const KParams &P, const float *act, const float q[9], Motor
         V3 t = p + mk(a[0] * 0.05f, a[1] * 0.05f, a[2] * 0.05f);
         t.z = fmaxf(0.0f, t.z);
         float qik[9];
-#ifndef PS_DBG_NO_IK
         inverse_kinematics<11>(q, t - P.sc.base, Q4{1.0f, 0.0f, 0.0f, 0.0f}, qik);
-#else
-        for (int d = 0; d < 9; d++) qik[d] = q[d] + t.x;
-#endif
 #pragma unroll
         for (int d = 0; d < 7; d++) tq[d] = qik[d];
     } else {
@@ -272,34 +411,41 @@ __global__ __launch_bounds__(kBlock) void k_init_state(KParams P) {
     const StateView &s = P.s;
     for (int r = 0; r < PS_NUM_FLOAT_ROWS; r++) s.F(r, i) = 0.0f;
     s.F(PS_F_CQUAT + 3, i) = 1.0f;
+    s.F(PS_F_C2QUAT + 3, i) = 1.0f;
     for (int d = 0; d < 9; d++) {
         s.F(PS_F_MKD + d, i) = 1.0f;
         s.F(PS_F_MIMP + d, i) = (float)PM_DEFAULT_MOTOR_MAX_IMPULSE;
     }
-    for (int d = 0; d < 3; d++) s.goal[d * s.stride + i] = 0.0;
+    for (int d = 0; d < PS_MAX_GOAL_DIM; d++) s.G(d, i) = 0.0;
     store_rng(s, i, pcg_seed(0));
+    aux_rng(s, i) = aux_seed(0);
     s.elapsed[i] = 0;
 }
 
 template <int TASK>
 __global__ __launch_bounds__(kBlock) void k_reset(KParams P, const uint8_t *mask, const uint64_t *seeds, float *obs,
                                                   float *ag, float *dg) {
+    using T = TaskTraits<TASK>;
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n) return;
     if (mask && !mask[i]) return;
     const StateView &s = P.s;
     Pcg r = seeds ? pcg_seed(seeds[i]) : load_rng(s, i);
+    uint64_t aux = seeds ? aux_seed(seeds[i]) : aux_rng(s, i);
     float q[9], qd[9];
-    Cube cb;
-    load_cube(s, i, cb);
-    double g[3];
-    reset_env<TASK>(P, i, q, qd, cb, g, r);
+    Body bd[T::NOBJ > 0 ? T::NOBJ : 1];
+#pragma unroll
+    for (int b = 0; b < T::NOBJ; b++) load_body(s, i, b, bd[b]);
+    double g[6] = {0, 0, 0, 0, 0, 0};
+    reset_env<TASK>(q, qd, bd, g, r, aux);
     store_robot(s, i, q, qd);
-    if constexpr (TASK != PS_TASK_REACH) store_cube(s, i, cb);
-    for (int d = 0; d < 3; d++) s.goal[d * s.stride + i] = g[d];
+#pragma unroll
+    for (int b = 0; b < T::NOBJ; b++) store_body(s, i, b, bd[b]);
+    for (int d = 0; d < T::GOAL; d++) s.G(d, i) = g[d];
     store_rng(s, i, r);
+    aux_rng(s, i) = aux;
     s.elapsed[i] = 0;
-    write_obs<TASK>(P, i, q, qd, cb, g, obs, ag, dg);
+    write_obs<TASK>(P, i, q, qd, bd, g, obs, ag, dg);
 }
 
 // The fused env step: one lane = one env = one full RobotTaskEnv.step().
@@ -307,19 +453,20 @@ template <int TASK, int CONTROL>
 __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions, float *obs, float *ag, float *dg,
                                                  float *reward, uint8_t *terminated, uint8_t *truncated,
                                                  float *final_obs, float *final_ag) {
+    using T = TaskTraits<TASK>;
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n) return;
     const StateView &s = P.s;
-    constexpr bool HAS_CUBE = TASK != PS_TASK_REACH;
 #ifdef PS_PROFILE_PHASES
     PhaseTimer pt;
     pt.last = __builtin_amdgcn_s_memtime();
-    for (int k = 0; k < PS_NUM_PHASES; k++) pt.acc[k] = 0;
+    for (int k = 0; k < PS_NUM_PROF_SLOTS; k++) pt.acc[k] = 0;
 #endif
     float q[9], qd[9];
     load_robot(s, i, q, qd);
-    Cube cb;
-    if constexpr (HAS_CUBE) load_cube(s, i, cb);
+    Body bd[T::NOBJ > 0 ? T::NOBJ : 1];
+#pragma unroll
+    for (int b = 0; b < T::NOBJ; b++) load_body(s, i, b, bd[b]);
     {
         Motors m;
         set_action<CONTROL>(P, actions + i * P.action_dim, q, m);
@@ -328,64 +475,65 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
     PS_PHASE(6);
     __shared__ float smem[LDS_FLOATS * kBlock];
     MJStore lds{(lds_float *)(smem + threadIdx.x), kBlock};
-    run_substeps<HAS_CUBE, true>(P, i, PM_SUBSTEPS, q, qd, cb, lds PS_PROF_ARG);
-    double g[3] = {s.goal[i], s.goal[s.stride + i], s.goal[2 * s.stride + i]};
-    // obs of the stepped state
-    float a0, a1, a2;
-    {
-        V3 p, v;
-        ee_state(P.sc, q, qd, p, v);
-        a0 = HAS_CUBE ? cb.pos.x : p.x;
-        a1 = HAS_CUBE ? cb.pos.y : p.y;
-        a2 = HAS_CUBE ? cb.pos.z : p.z;
-    }
-    double dist = goal_distance(a0, a1, a2, g[0], g[1], g[2]);
-    bool term = dist < PM_DISTANCE_THRESHOLD;
+    run_substeps<T::NOBJ, T::SHAPE, true>(P, i, PM_SUBSTEPS, q, qd, bd, lds PS_PROF_ARG);
+    double g[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int d = 0; d < T::GOAL; d++) g[d] = s.G(d, i);
+    float a[6];
+    achieved<TASK>(P, q, qd, bd, a);
+    double dist = goal_metric<TASK>(a, g);
+    bool term = dist < T::THRESHOLD;
     int el = s.elapsed[i] + 1;
-    bool trunc = el >= PM_MAX_EPISODE_STEPS;
-    reward[i] = reward_of(P.reward_type, dist);
+    bool trunc = el >= T::STEPS;
+    reward[i] = reward_for(P.reward_type, dist, T::THRESHOLD);
     terminated[i] = term;
     truncated[i] = trunc;
     if (P.autoreset && (term || trunc)) {
-        if (final_obs || final_ag) write_obs<TASK>(P, i, q, qd, cb, g, final_obs, final_ag, nullptr);
+        if (final_obs || final_ag) write_obs<TASK>(P, i, q, qd, bd, g, final_obs, final_ag, nullptr);
         Pcg r = load_rng(s, i);
-        reset_env<TASK>(P, i, q, qd, cb, g, r);
+        uint64_t aux = aux_rng(s, i);
+        reset_env<TASK>(q, qd, bd, g, r, aux);
         store_rng(s, i, r);
-        for (int d = 0; d < 3; d++) s.goal[d * s.stride + i] = g[d];
+        aux_rng(s, i) = aux;
+        for (int d = 0; d < T::GOAL; d++) s.G(d, i) = g[d];
         el = 0;
     } else if (final_obs || final_ag) {
-        write_obs<TASK>(P, i, q, qd, cb, g, final_obs, final_ag, nullptr);
+        write_obs<TASK>(P, i, q, qd, bd, g, final_obs, final_ag, nullptr);
     }
     s.elapsed[i] = el;
     store_robot(s, i, q, qd);
-    if constexpr (HAS_CUBE) store_cube(s, i, cb);
-    write_obs<TASK>(P, i, q, qd, cb, g, obs, ag, dg);
+#pragma unroll
+    for (int b = 0; b < T::NOBJ; b++) store_body(s, i, b, bd[b]);
+    write_obs<TASK>(P, i, q, qd, bd, g, obs, ag, dg);
 #ifdef PS_PROFILE_PHASES
     PS_PHASE(7);
     if ((threadIdx.x & 63) == 0)
-        for (int k = 0; k < PS_NUM_PHASES; k++) atomicAdd((unsigned long long *)&ps_phase_cycles[k], (unsigned long long)pt.acc[k]);
+        for (int k = 0; k < PS_NUM_PROF_SLOTS; k++)
+            atomicAdd((unsigned long long *)&ps_phase_cycles[k], (unsigned long long)pt.acc[k]);
 #endif
 }
 
-template <bool HAS_CUBE>
+template <int NOBJ, int SHAPE>
 __global__ __launch_bounds__(kBlock) void k_sim_step(KParams P, int n_substeps) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n) return;
     const StateView &s = P.s;
     float q[9], qd[9];
     load_robot(s, i, q, qd);
-    Cube cb;
-    if constexpr (HAS_CUBE) load_cube(s, i, cb);
+    Body bd[NOBJ > 0 ? NOBJ : 1];
+#pragma unroll
+    for (int b = 0; b < NOBJ; b++) load_body(s, i, b, bd[b]);
     __shared__ float smem[LDS_FLOATS * kBlock];
     MJStore lds{(lds_float *)(smem + threadIdx.x), kBlock};
 #ifdef PS_PROFILE_PHASES
     PhaseTimer pt;
     pt.last = __builtin_amdgcn_s_memtime();
-    for (int k = 0; k < PS_NUM_PHASES; k++) pt.acc[k] = 0;
+    for (int k = 0; k < PS_NUM_PROF_SLOTS; k++) pt.acc[k] = 0;
 #endif
-    run_substeps<HAS_CUBE, false>(P, i, n_substeps, q, qd, cb, lds PS_PROF_ARG);
+    run_substeps<NOBJ, SHAPE, false>(P, i, n_substeps, q, qd, bd, lds PS_PROF_ARG);
     store_robot(s, i, q, qd);
-    if constexpr (HAS_CUBE) store_cube(s, i, cb);
+#pragma unroll
+    for (int b = 0; b < NOBJ; b++) store_body(s, i, b, bd[b]);
 }
 
 __global__ __launch_bounds__(kBlock) void k_link_state(KParams P, int link, float *pos, float *quat, float *lv,
@@ -398,13 +546,11 @@ __global__ __launch_bounds__(kBlock) void k_link_state(KParams P, int link, floa
     fk(q, k);
     // COM frame of `link` (getLinkState [0], [1], [6], [7])
     M3 R = k.f[0].R;
-    V3 o = k.f[0].o;
     V3 c = mk(0, 0, 0);
     static_for<0, PM_NUM_LINKS>([&](auto L) {
         constexpr int l = decltype(L)::value;
         if (l == link) {
             R = k.f[l].R;
-            o = k.f[l].o;
             c = com_pos<l>(k);
         }
     });
@@ -425,7 +571,6 @@ __global__ __launch_bounds__(kBlock) void k_link_state(KParams P, int link, floa
             }
         }
     });
-    (void)o;
     if (pos) { V3 p = c + P.sc.base; pos[i * 3] = p.x; pos[i * 3 + 1] = p.y; pos[i * 3 + 2] = p.z; }
     if (quat) { Q4 qq = mat_to_quat(R); quat[i * 4] = qq.x; quat[i * 4 + 1] = qq.y; quat[i * 4 + 2] = qq.z; quat[i * 4 + 3] = qq.w; }
     if (lv) { lv[i * 3] = v.x; lv[i * 3 + 1] = v.y; lv[i * 3 + 2] = v.z; }
@@ -446,11 +591,13 @@ __global__ __launch_bounds__(kBlock) void k_ik(KParams P, const float *pos, cons
 }
 
 // gymnasium.utils.seeding.np_random(seed) per env (core.py:244): the env's
-// generator becomes Generator(PCG64(SeedSequence(seeds[i])))
+// generator becomes Generator(PCG64(SeedSequence(seeds[i]))), and Flip's goal
+// stream restarts from the same seed
 __global__ __launch_bounds__(kBlock) void k_rng_seed(KParams P, const uint8_t *mask, const uint64_t *seeds) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n || (mask && !mask[i])) return;
     store_rng(P.s, i, pcg_seed(seeds[i]));
+    aux_rng(P.s, i) = aux_seed(seeds[i]);
 }
 
 // Generator.uniform(low[n], high[n]) per env: n consecutive draws from the
@@ -467,14 +614,25 @@ __global__ __launch_bounds__(kBlock) void k_rng_uniform(KParams P, const uint8_t
     store_rng(P.s, i, r);
 }
 
+// Flip's goal (Rotation.random(), flip.py:70-72) from each env's goal stream
+__global__ __launch_bounds__(kBlock) void k_rng_rotation(KParams P, const uint8_t *mask, double *out) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n || (mask && !mask[i])) return;
+    uint64_t st = aux_rng(P.s, i);
+    double q[4];
+    random_rotation(st, q);
+    aux_rng(P.s, i) = st;
+    for (int k = 0; k < 4; k++) out[i * 4 + k] = q[k];
+}
+
 // getBasePositionAndOrientation + getEulerFromQuaternion + getBaseVelocity of
-// the object (pybullet.py:284-349)
-__global__ __launch_bounds__(kBlock) void k_base_state(KParams P, float *pos, float *quat, float *euler, float *vel,
-                                                       float *avel) {
+// object `b` (pybullet.py:284-349)
+__global__ __launch_bounds__(kBlock) void k_base_state(KParams P, int b, float *pos, float *quat, float *euler,
+                                                       float *vel, float *avel) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P.n) return;
-    Cube c;
-    load_cube(P.s, i, c);
+    Body c;
+    load_body(P.s, i, b, c);
     if (pos) { pos[i * 3] = c.pos.x; pos[i * 3 + 1] = c.pos.y; pos[i * 3 + 2] = c.pos.z; }
     if (quat) { quat[i * 4] = c.quat.x; quat[i * 4 + 1] = c.quat.y; quat[i * 4 + 2] = c.quat.z; quat[i * 4 + 3] = c.quat.w; }
     if (euler) { V3 e = euler_from_quat(c.quat); euler[i * 3] = e.x; euler[i * 3 + 1] = e.y; euler[i * 3 + 2] = e.z; }
@@ -482,25 +640,46 @@ __global__ __launch_bounds__(kBlock) void k_base_state(KParams P, float *pos, fl
     if (avel) { avel[i * 3] = c.omg.x; avel[i * 3 + 1] = c.omg.y; avel[i * 3 + 2] = c.omg.z; }
 }
 
-__global__ __launch_bounds__(256) void k_compute_reward(int reward_type, const void *ag, int ag_dbl, const void *dg,
-                                                        int dg_dbl, float *reward, uint8_t *success, int64_t n) {
+// compute_reward / is_success for HER (core.py:226): goal pairs of `gd`
+// values; f64 arithmetic when either side is f64 (numpy promotion), f32
+// otherwise (threshold rounded to f32)
+__global__ __launch_bounds__(256) void k_compute_reward(int task, int reward_type, const void *ag, int ag_dbl,
+                                                        const void *dg, int dg_dbl, float *reward, uint8_t *success,
+                                                        int64_t n) {
+#pragma clang fp contract(off)
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    const int gd = task == PS_TASK_STACK ? 6 : (task == PS_TASK_FLIP ? 4 : 3);
+    const bool angle = task == PS_TASK_FLIP;
+    const double thr = task == PS_TASK_STACK ? PM_STACK_DISTANCE_THRESHOLD
+                       : angle                ? PM_FLIP_DISTANCE_THRESHOLD
+                                              : PM_DISTANCE_THRESHOLD;
     if (ag_dbl || dg_dbl) {
-        // numpy promotes the mixed pair to float64 (utils.py:15)
-        double a[3], g[3];
-        for (int k = 0; k < 3; k++) {
-            a[k] = ag_dbl ? ((const double *)ag)[i * 3 + k] : (double)((const float *)ag)[i * 3 + k];
-            g[k] = dg_dbl ? ((const double *)dg)[i * 3 + k] : (double)((const float *)dg)[i * 3 + k];
+        double m = 0.0;
+        for (int k = 0; k < gd; k++) {
+            double a = ag_dbl ? ((const double *)ag)[i * gd + k] : (double)((const float *)ag)[i * gd + k];
+            double g = dg_dbl ? ((const double *)dg)[i * gd + k] : (double)((const float *)dg)[i * gd + k];
+            double e = __dsub_rn(a, g);
+            double t = angle ? opaque(__dmul_rn(a, g)) : opaque(__dmul_rn(e, e));
+            m = k == 0 ? t : __dadd_rn(m, t);
         }
-        double dist = goal_distance_f64(a[0], a[1], a[2], g[0], g[1], g[2]);
-        if (reward) reward[i] = reward_of(reward_type, dist);
-        if (success) success[i] = dist < PM_DISTANCE_THRESHOLD;
+        double d = angle ? __dsub_rn(1.0, opaque(__dmul_rn(m, m))) : __dsqrt_rn(m);
+        if (reward) reward[i] = reward_for(reward_type, d, thr);
+        if (success) success[i] = d < thr;
     } else {
         const float *a = (const float *)ag, *g = (const float *)dg;
-        float dist = goal_distance_f32(a[i * 3], a[i * 3 + 1], a[i * 3 + 2], g[i * 3], g[i * 3 + 1], g[i * 3 + 2]);
-        if (reward) reward[i] = reward_of_f32(reward_type, dist);
-        if (success) success[i] = dist < (float)PM_DISTANCE_THRESHOLD;
+        float m = 0.0f;
+        for (int k = 0; k < gd; k++) {
+            float av = a[i * gd + k], gv = g[i * gd + k];
+            float e = __fsub_rn(av, gv);
+            float t = angle ? opaque(__fmul_rn(av, gv)) : opaque(__fmul_rn(e, e));
+            m = k == 0 ? t : __fadd_rn(m, t);
+        }
+        // correctly rounded f32 root: the f64 root rounded once
+        float d = angle ? __fsub_rn(1.0f, opaque(__fmul_rn(m, m))) : __double2float_rn(__dsqrt_rn((double)m));
+        float tf = (float)thr;
+        if (reward) reward[i] = reward_type == 0 ? (d > tf ? -1.0f : -0.0f) : -d;
+        if (success) success[i] = d < tf;
     }
 }
 
@@ -534,6 +713,12 @@ KParams params_of(ps_ctx *c, void *state) {
 
 dim3 grid_of(int64_t n, int block) { return dim3((unsigned)((n + block - 1) / block)); }
 
+// the registered scene of each task (its _create_scene + panda_tasks.py)
+bool scene_matches_task(const ps_config &c) {
+    return c.n_objects == task_nobj(c.task) &&
+           (c.n_objects == 0 || c.object_shape == (c.task == PS_TASK_SLIDE ? PS_SHAPE_CYLINDER : PS_SHAPE_BOX));
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------- C ABI
@@ -542,18 +727,34 @@ extern "C" {
 int ps_abi_version(void) { return PS_ABI_VERSION; }
 
 int ps_default_config(int task, int control, int reward, ps_config *out) {
-    if (!out || task < 0 || task > 2 || control < 0 || control > 1 || reward < 0 || reward > 1) return PS_ERR_ARG;
+    if (!out || task < 0 || task >= PS_NUM_TASKS || control < 0 || control > 1 || reward < 0 || reward > 1)
+        return PS_ERR_ARG;
     memset(out, 0, sizeof *out);
     out->task = task;
     out->control = control;
     out->reward = reward;
-    out->block_gripper = task != PS_TASK_PICK_AND_PLACE;
+    // Reach/Push/Slide block the gripper (panda_tasks.py:62,78,94)
+    out->block_gripper = task == PS_TASK_REACH || task == PS_TASK_PUSH || task == PS_TASK_SLIDE;
     out->has_table = 1;
     out->has_plane = 1;
-    out->has_cube = task != PS_TASK_REACH;
+    out->n_objects = task_nobj(task);
+    out->object_shape = task == PS_TASK_SLIDE ? PS_SHAPE_CYLINDER : PS_SHAPE_BOX;
     out->base[0] = (float)PM_BASE_X;
-    out->cube_half = (float)PM_CUBE_HALF;
-    out->cube_mass = (float)PM_CUBE_MASS;
+    if (task == PS_TASK_SLIDE) {
+        out->object_half[0] = out->object_half[1] = (float)(PM_SLIDE_OBJECT_SIZE / 2);
+        out->object_half[2] = (float)(PM_SLIDE_OBJECT_SIZE / 2 / 2);
+        out->object_friction = (float)PM_SLIDE_FRICTION;
+        out->table_cx = (float)PM_SLIDE_TABLE_CX;
+        out->table_hx = (float)PM_SLIDE_TABLE_HX;
+    } else {
+        out->object_half[0] = out->object_half[1] = out->object_half[2] = (float)(PM_OBJECT_SIZE / 2);
+        out->object_friction = (float)PM_DEFAULT_FRICTION;
+        out->table_cx = (float)PM_TABLE_CX;
+        out->table_hx = (float)PM_TABLE_HX;
+    }
+    out->table_hy = (float)PM_TABLE_HY;
+    out->object_mass = (float)(task == PS_TASK_STACK ? PM_STACK_MASS1 : PM_CUBE_MASS);
+    out->object2_mass = (float)PM_STACK_MASS2;
     return PS_OK;
 }
 
@@ -564,17 +765,27 @@ int ps_state_layout(int64_t num_envs, ps_layout *out) {
     out->stride = stride;
     out->float_offset = 0;
     out->goal_offset = out->float_offset + (int64_t)PS_NUM_FLOAT_ROWS * stride * 4;
-    out->rng_offset = out->goal_offset + 3 * stride * 8;
-    out->elapsed_offset = out->rng_offset + 4 * stride * 8;
+    out->rng_offset = out->goal_offset + (int64_t)PS_MAX_GOAL_DIM * stride * 8;
+    out->elapsed_offset = out->rng_offset + (int64_t)PS_NUM_RNG_ROWS * stride * 8;
     out->total_bytes = out->elapsed_offset + stride * 4;
     return PS_OK;
 }
 
 int ps_create(const ps_config *cfg, int64_t num_envs, int device, ps_ctx **out) {
     if (!cfg || !out || num_envs <= 0) return PS_ERR_ARG;
-    if (cfg->task < 0 || cfg->task > 2 || cfg->control < 0 || cfg->control > 1 || cfg->reward < 0 || cfg->reward > 1)
+    if (cfg->task < 0 || cfg->task >= PS_NUM_TASKS || cfg->control < 0 || cfg->control > 1 || cfg->reward < 0 ||
+        cfg->reward > 1 || cfg->n_objects < 0 || cfg->n_objects > 2 || cfg->object_shape < 0 || cfg->object_shape > 1)
         return PS_ERR_ARG;
-    if ((cfg->task == PS_TASK_REACH) == (cfg->has_cube != 0)) return PS_ERR_UNSUPPORTED;
+    if (cfg->n_objects > 0) {
+        // compiled-in shapes: cubes (isotropic), one upright z cylinder
+        if (cfg->object_shape == PS_SHAPE_BOX &&
+            (cfg->object_half[0] != cfg->object_half[1] || cfg->object_half[1] != cfg->object_half[2]))
+            return PS_ERR_UNSUPPORTED;
+        if (cfg->object_shape == PS_SHAPE_CYLINDER &&
+            (cfg->n_objects != 1 || cfg->object_half[0] != cfg->object_half[1]))
+            return PS_ERR_UNSUPPORTED;
+        if (!(cfg->object_mass > 0.0f) || (cfg->n_objects == 2 && !(cfg->object2_mass > 0.0f))) return PS_ERR_ARG;
+    }
     ps_ctx *c = new (std::nothrow) ps_ctx;
     if (!c) return PS_ERR_ARG;
     memset(c, 0, sizeof *c);
@@ -590,13 +801,16 @@ void ps_destroy(ps_ctx *ctx) { delete ctx; }
 
 const char *ps_last_error(const ps_ctx *ctx) { return ctx ? ctx->err : "null context"; }
 
-int ps_obs_dim(const ps_ctx *c) {
-    int robot = c->cfg.block_gripper ? 6 : 7;
-    return robot + (c->cfg.task == PS_TASK_REACH ? 0 : 12);
-}
+int ps_obs_dim(const ps_ctx *c) { return (c->cfg.block_gripper ? 6 : 7) + task_obs_dim(c->cfg.task); }
 
 int ps_action_dim(const ps_ctx *c) {
     return (c->cfg.control == PS_CONTROL_EE ? 3 : 7) + (c->cfg.block_gripper ? 0 : 1);
+}
+
+int ps_goal_dim(const ps_ctx *c) { return task_goal_dim(c->cfg.task); }
+
+int ps_max_episode_steps(const ps_ctx *c) {
+    return c->cfg.task == PS_TASK_STACK ? PM_STACK_MAX_EPISODE_STEPS : PM_MAX_EPISODE_STEPS;
 }
 
 int ps_init_state(ps_ctx *c, void *state, void *stream) {
@@ -609,14 +823,20 @@ int ps_init_state(ps_ctx *c, void *state, void *stream) {
 int ps_reset(ps_ctx *c, void *state, const uint8_t *mask, const uint64_t *seeds, float *obs, float *ag, float *dg,
              void *stream) {
     if (!c || !state) return fail(c, PS_ERR_ARG, "null argument");
+    if (!scene_matches_task(c->cfg)) return fail(c, PS_ERR_UNSUPPORTED, "scene does not match the task");
     KParams P = params_of(c, state);
     dim3 g = grid_of(P.n, kBlock), b(kBlock);
     hipStream_t st = (hipStream_t)stream;
+#define PS_LAUNCH_RESET(T) hipLaunchKernelGGL(k_reset<T>, g, b, 0, st, P, mask, seeds, obs, ag, dg)
     switch (c->cfg.task) {
-        case PS_TASK_REACH: hipLaunchKernelGGL(k_reset<PS_TASK_REACH>, g, b, 0, st, P, mask, seeds, obs, ag, dg); break;
-        case PS_TASK_PUSH: hipLaunchKernelGGL(k_reset<PS_TASK_PUSH>, g, b, 0, st, P, mask, seeds, obs, ag, dg); break;
-        default: hipLaunchKernelGGL(k_reset<PS_TASK_PICK_AND_PLACE>, g, b, 0, st, P, mask, seeds, obs, ag, dg); break;
+        case PS_TASK_REACH: PS_LAUNCH_RESET(PS_TASK_REACH); break;
+        case PS_TASK_PUSH: PS_LAUNCH_RESET(PS_TASK_PUSH); break;
+        case PS_TASK_PICK_AND_PLACE: PS_LAUNCH_RESET(PS_TASK_PICK_AND_PLACE); break;
+        case PS_TASK_SLIDE: PS_LAUNCH_RESET(PS_TASK_SLIDE); break;
+        case PS_TASK_STACK: PS_LAUNCH_RESET(PS_TASK_STACK); break;
+        default: PS_LAUNCH_RESET(PS_TASK_FLIP); break;
     }
+#undef PS_LAUNCH_RESET
     return check_launch(c);
 }
 
@@ -625,25 +845,26 @@ int ps_step(ps_ctx *c, void *state, const float *actions, float *obs, float *ag,
             void *stream) {
     if (!c || !state || !actions || !reward || !terminated || !truncated)
         return fail(c, PS_ERR_ARG, "null argument");
+    if (!scene_matches_task(c->cfg)) return fail(c, PS_ERR_UNSUPPORTED, "scene does not match the task");
     KParams P = params_of(c, state);
     P.autoreset = autoreset;
     dim3 g = grid_of(P.n, kBlock), b(kBlock);
     hipStream_t st = (hipStream_t)stream;
-#define PS_LAUNCH_STEP(T, C) \
-    hipLaunchKernelGGL((k_step<T, C>), g, b, 0, st, P, actions, obs, ag, dg, reward, terminated, truncated, final_obs, final_ag)
-    int ee = c->cfg.control == PS_CONTROL_EE;
+#define PS_LAUNCH_STEP(T, C)                                                                                     \
+    hipLaunchKernelGGL((k_step<T, C>), g, b, 0, st, P, actions, obs, ag, dg, reward, terminated, truncated, \
+                       final_obs, final_ag)
+#define PS_LAUNCH_TASK(T)                                                  \
+    if (c->cfg.control == PS_CONTROL_EE) PS_LAUNCH_STEP(T, PS_CONTROL_EE); \
+    else PS_LAUNCH_STEP(T, PS_CONTROL_JOINTS);
     switch (c->cfg.task) {
-        case PS_TASK_REACH:
-            if (ee) PS_LAUNCH_STEP(PS_TASK_REACH, PS_CONTROL_EE); else PS_LAUNCH_STEP(PS_TASK_REACH, PS_CONTROL_JOINTS);
-            break;
-        case PS_TASK_PUSH:
-            if (ee) PS_LAUNCH_STEP(PS_TASK_PUSH, PS_CONTROL_EE); else PS_LAUNCH_STEP(PS_TASK_PUSH, PS_CONTROL_JOINTS);
-            break;
-        default:
-            if (ee) PS_LAUNCH_STEP(PS_TASK_PICK_AND_PLACE, PS_CONTROL_EE);
-            else PS_LAUNCH_STEP(PS_TASK_PICK_AND_PLACE, PS_CONTROL_JOINTS);
-            break;
+        case PS_TASK_REACH: PS_LAUNCH_TASK(PS_TASK_REACH); break;
+        case PS_TASK_PUSH: PS_LAUNCH_TASK(PS_TASK_PUSH); break;
+        case PS_TASK_PICK_AND_PLACE: PS_LAUNCH_TASK(PS_TASK_PICK_AND_PLACE); break;
+        case PS_TASK_SLIDE: PS_LAUNCH_TASK(PS_TASK_SLIDE); break;
+        case PS_TASK_STACK: PS_LAUNCH_TASK(PS_TASK_STACK); break;
+        default: PS_LAUNCH_TASK(PS_TASK_FLIP); break;
     }
+#undef PS_LAUNCH_TASK
 #undef PS_LAUNCH_STEP
     return check_launch(c);
 }
@@ -652,8 +873,12 @@ int ps_sim_step(ps_ctx *c, void *state, int n_substeps, void *stream) {
     if (!c || !state || n_substeps < 0) return fail(c, PS_ERR_ARG, "bad argument");
     KParams P = params_of(c, state);
     dim3 g = grid_of(P.n, kBlock), b(kBlock);
-    if (c->cfg.has_cube) hipLaunchKernelGGL(k_sim_step<true>, g, b, 0, (hipStream_t)stream, P, n_substeps);
-    else hipLaunchKernelGGL(k_sim_step<false>, g, b, 0, (hipStream_t)stream, P, n_substeps);
+    hipStream_t st = (hipStream_t)stream;
+    if (c->cfg.n_objects == 0) hipLaunchKernelGGL((k_sim_step<0, PS_SHAPE_BOX>), g, b, 0, st, P, n_substeps);
+    else if (c->cfg.n_objects == 2) hipLaunchKernelGGL((k_sim_step<2, PS_SHAPE_BOX>), g, b, 0, st, P, n_substeps);
+    else if (c->cfg.object_shape == PS_SHAPE_CYLINDER)
+        hipLaunchKernelGGL((k_sim_step<1, PS_SHAPE_CYLINDER>), g, b, 0, st, P, n_substeps);
+    else hipLaunchKernelGGL((k_sim_step<1, PS_SHAPE_BOX>), g, b, 0, st, P, n_substeps);
     return check_launch(c);
 }
 
@@ -705,21 +930,29 @@ int ps_rng_uniform(ps_ctx *c, void *state, const uint8_t *mask, int n, const dou
     return check_launch(c);
 }
 
-int ps_base_state(ps_ctx *c, const void *state, float *pos, float *quat, float *euler, float *lin_vel,
-                  float *ang_vel, void *stream) {
-    if (!c || !state) return fail(c, PS_ERR_ARG, "null argument");
-    if (!c->cfg.has_cube) return fail(c, PS_ERR_UNSUPPORTED, "scene has no object");
-    KParams P = params_of(c, (void *)state);
-    hipLaunchKernelGGL(k_base_state, grid_of(P.n, kBlock), dim3(kBlock), 0, (hipStream_t)stream, P, pos, quat, euler,
-                       lin_vel, ang_vel);
+int ps_rng_rotation(ps_ctx *c, void *state, const uint8_t *mask, double *out, void *stream) {
+    if (!c || !state || !out) return fail(c, PS_ERR_ARG, "null argument");
+    KParams P = params_of(c, state);
+    hipLaunchKernelGGL(k_rng_rotation, grid_of(P.n, kBlock), dim3(kBlock), 0, (hipStream_t)stream, P, mask, out);
     return check_launch(c);
 }
 
-int ps_compute_reward(int reward_type, const void *ag, int ag_is_double, const void *dg, int dg_is_double,
+int ps_base_state(ps_ctx *c, const void *state, int object, float *pos, float *quat, float *euler, float *lin_vel,
+                  float *ang_vel, void *stream) {
+    if (!c || !state) return fail(c, PS_ERR_ARG, "null argument");
+    if (object < 0 || object >= c->cfg.n_objects) return fail(c, PS_ERR_UNSUPPORTED, "scene has no such object");
+    KParams P = params_of(c, (void *)state);
+    hipLaunchKernelGGL(k_base_state, grid_of(P.n, kBlock), dim3(kBlock), 0, (hipStream_t)stream, P, object, pos,
+                       quat, euler, lin_vel, ang_vel);
+    return check_launch(c);
+}
+
+int ps_compute_reward(int task, int reward_type, const void *ag, int ag_is_double, const void *dg, int dg_is_double,
                       float *reward, uint8_t *success, int64_t n, void *stream) {
-    if (!ag || !dg || n < 0 || reward_type < 0 || reward_type > 1) return PS_ERR_ARG;
+    if (!ag || !dg || n < 0 || task < 0 || task >= PS_NUM_TASKS || reward_type < 0 || reward_type > 1)
+        return PS_ERR_ARG;
     if (n == 0) return PS_OK;
-    hipLaunchKernelGGL(k_compute_reward, grid_of(n, 256), dim3(256), 0, (hipStream_t)stream, reward_type, ag,
+    hipLaunchKernelGGL(k_compute_reward, grid_of(n, 256), dim3(256), 0, (hipStream_t)stream, task, reward_type, ag,
                        ag_is_double, dg, dg_is_double, reward, success, n);
     return hipGetLastError() == hipSuccess ? PS_OK : PS_ERR_HIP;
 }

@@ -10,6 +10,7 @@
 #include <type_traits>
 
 #include "panda_model.h"
+#include "pandasim.h"
 
 #define PS_D __device__ __forceinline__
 #define PS_HD __host__ __device__ __forceinline__
@@ -18,9 +19,10 @@
 // each wave accumulates s_memtime deltas per phase and lane 0 adds them to
 // ps_phase_cycles at the end of the kernel.  Compiled out of the product.
 #define PS_NUM_PHASES 8
+#define PS_NUM_PROF_SLOTS 12  // phases + PGS counters (lane iterations, wave iterations, substeps, robot-contact slots run)
 #ifdef PS_PROFILE_PHASES
 struct PhaseTimer {
-    uint64_t last, acc[PS_NUM_PHASES];
+    uint64_t last, acc[PS_NUM_PROF_SLOTS];
 };
 #define PS_PROF_PARAM , PhaseTimer &pt
 #define PS_PROF_ARG , pt

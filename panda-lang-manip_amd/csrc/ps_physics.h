@@ -379,24 +379,70 @@ PS_D void inverse_kinematics(const float q_start[9], V3 target, Q4 orn, float q_
 }
 
 // ------------------------------------------------------------- the scene
+// Objects: NOBJ dynamic bodies (0 Reach; 1 Push/PickAndPlace/Flip/Slide; 2
+// Stack) of one SHAPE (SHAPE_BOX: cubes, isotropic inertia; SHAPE_CYL: the
+// upright cylinder of Slide, anisotropic inertia).
+constexpr int SHAPE_BOX = PS_SHAPE_BOX;
+constexpr int SHAPE_CYL = PS_SHAPE_CYLINDER;
+
 struct Scene {
     V3 base;
-    float half, mass;
-    int has_table, has_plane, has_cube;
+    V3 half;                 // box half extents; cylinder (radius, radius, half height)
+    float mass, mass2, fric;  // object 1 / object 2 mass, lateral friction of the objects
+    float table_cx, table_hx, table_hy;
+    int has_table, has_plane;
 };
 
 struct Motors {
     float target[9], kp[9], kd[9], vel[9], imp[9];
 };
 
-struct Cube {
+struct Body {
     V3 pos;
     Q4 quat;
     V3 vel, omg;
 };
+typedef Body Cube;
+
+// btBoxShape / btCylinderShapeZ::calculateLocalInertia (oracle object_inertia)
+template <int SHAPE>
+PS_D V3 local_inertia(const Scene &sc, float m) {
+    if constexpr (SHAPE == SHAPE_CYL) {
+        float r = sc.half.x, hh = sc.half.z;
+        float t1 = m / 12.0f * (4.0f * hh * hh) + m / 4.0f * (r * r), t2 = m / 2.0f * (r * r);
+        return mk(t1, t1, t2);
+    } else {
+        float lx = 2.0f * sc.half.x, ly = 2.0f * sc.half.y, lz = 2.0f * sc.half.z;
+        return mk(m / 12.0f * (ly * ly + lz * lz), m / 12.0f * (lx * lx + lz * lz), m / 12.0f * (lx * lx + ly * ly));
+    }
+}
+
+// per-substep body quantities: the world inverse inertia is a scalar for the
+// isotropic cubes and a symmetric 3x3 for the cylinder
+template <int SHAPE>
+struct BodyDyn {
+    M3 R;
+    float inv_m, iI;
+    S3 Ii;
+    PS_D V3 inv_inertia(V3 v) const {
+        if constexpr (SHAPE == SHAPE_CYL) return mul(Ii, v);
+        else return v * iI;
+    }
+};
+
+template <int SHAPE>
+PS_D BodyDyn<SHAPE> body_dyn(const Scene &sc, const Body &b, float m) {
+    BodyDyn<SHAPE> o;
+    o.R = quat_to_mat(b.quat);
+    o.inv_m = 1.0f / m;
+    V3 I = local_inertia<SHAPE>(sc, m);
+    o.iI = 1.0f / I.x;
+    if constexpr (SHAPE == SHAPE_CYL) o.Ii = rotate_diag(o.R, 1.0f / I.x, 1.0f / I.y, 1.0f / I.z);
+    return o;
+}
 
 PS_D bool ground_top(const Scene &sc, float x, float y, float &top) {
-    if (sc.has_table && fabsf(x - (float)PM_TABLE_CX) <= (float)PM_TABLE_HX && fabsf(y) <= (float)PM_TABLE_HY) {
+    if (sc.has_table && fabsf(x - sc.table_cx) <= sc.table_hx && fabsf(y) <= sc.table_hy) {
         top = (float)PM_TABLE_TOP;
         return true;
     }
@@ -405,6 +451,76 @@ PS_D bool ground_top(const Scene &sc, float x, float y, float &top) {
         return true;
     }
     return false;
+}
+
+// support point v of the shape (object frame): box vertices, or cylinder rim
+// points (bottom cap then top cap, PM_CYL_RIM_ORDER)
+template <int SHAPE>
+constexpr int num_support() { return SHAPE == SHAPE_CYL ? 2 * PM_CYL_RIM_POINTS : 8; }
+
+template <int SHAPE, int V>
+PS_D V3 support_point(const Scene &sc) {
+    if constexpr (SHAPE == SHAPE_CYL) {
+        constexpr int order[PM_CYL_RIM_POINTS] = PM_CYL_RIM_ORDER;
+        constexpr int cap = V / PM_CYL_RIM_POINTS;
+        constexpr int j = order[V % PM_CYL_RIM_POINTS];
+        // cos/sin of multiples of 45 degrees, exact to float
+        constexpr float cs[8] = {1.0f, 0.70710678118654752f, 0.0f, -0.70710678118654752f,
+                                 -1.0f, -0.70710678118654752f, 0.0f, 0.70710678118654752f};
+        constexpr float sn[8] = {0.0f, 0.70710678118654752f, 1.0f, 0.70710678118654752f,
+                                 0.0f, -0.70710678118654752f, -1.0f, -0.70710678118654752f};
+        return mk(sc.half.x * cs[j], sc.half.x * sn[j], cap ? sc.half.z : -sc.half.z);
+    } else {
+        return mk((V & 1) ? sc.half.x : -sc.half.x, (V & 2) ? sc.half.y : -sc.half.y,
+                  (V & 4) ? sc.half.z : -sc.half.z);
+    }
+}
+
+// closest point of the solid to `loc` (object frame): surface point cl,
+// outward normal nl; returns the signed distance (negative inside)
+template <int SHAPE>
+PS_D float object_closest(const Scene &sc, V3 loc, V3 &cl, V3 &nl) {
+    const V3 h = sc.half;
+    if constexpr (SHAPE == SHAPE_CYL) {
+        float r = h.x, hh = h.z;
+        float rho = sqrtf(loc.x * loc.x + loc.y * loc.y);
+        float zc = fminf(fmaxf(loc.z, -hh), hh);
+        float s = rho > r ? r / rho : 1.0f;
+        cl = mk(loc.x * s, loc.y * s, zc);
+        V3 dif = loc - cl;
+        float dn = norm(dif);
+        if (dn > 1e-9f) {
+            nl = dif * (1.0f / dn);
+            return dn;
+        }
+        float side = r - rho, cap = hh - fabsf(loc.z);
+        if (side < cap) {
+            nl = rho > 1e-12f ? mk(loc.x / rho, loc.y / rho, 0.0f) : mk(1.0f, 0.0f, 0.0f);
+            cl = mk(nl.x * r, nl.y * r, cl.z);
+            return -side;
+        }
+        nl = mk(0.0f, 0.0f, loc.z >= 0.0f ? 1.0f : -1.0f);
+        cl.z = nl.z * hh;
+        return -cap;
+    } else {
+        cl = mk(fminf(fmaxf(loc.x, -h.x), h.x), fminf(fmaxf(loc.y, -h.y), h.y), fminf(fmaxf(loc.z, -h.z), h.z));
+        V3 dif = loc - cl;
+        float dn = norm(dif);
+        if (dn > 1e-9f) {
+            nl = dif * (1.0f / dn);
+            return dn;
+        }
+        float bx = h.x - fabsf(loc.x), by = h.y - fabsf(loc.y), bz = h.z - fabsf(loc.z);
+        int ax = 0;
+        float best = bx;
+        if (by < best) { best = by; ax = 1; }
+        if (bz < best) { best = bz; ax = 2; }
+        float sg;
+        if (ax == 0) { sg = loc.x >= 0.0f ? 1.0f : -1.0f; nl = mk(sg, 0, 0); cl.x = sg * h.x; }
+        else if (ax == 1) { sg = loc.y >= 0.0f ? 1.0f : -1.0f; nl = mk(0, sg, 0); cl.y = sg * h.y; }
+        else { sg = loc.z >= 0.0f ? 1.0f : -1.0f; nl = mk(0, 0, sg); cl.z = sg * h.z; }
+        return -best;
+    }
 }
 
 // btPlaneSpace1
@@ -422,11 +538,12 @@ PS_D void plane_space(V3 n, V3 &p, V3 &q) {
 
 constexpr int NG = PM_MAX_GROUND_CONTACTS;
 constexpr int NR = PM_MAX_ROBOT_CONTACTS;
+constexpr int NP = PM_MAX_PAIR_CONTACTS;
 // LDS floats per lane: M^-1 J^T of the 3 rows of every gripper contact
 // (108 floats x 256 lanes per CU = 108 KiB of the 160 KiB LDS at one wave per
 // SIMD); the diagnostic PS_MI_LDS build appends the packed M^-1.
 // Then 40 floats of per-substep values the PGS loop never reads (q, v1, the
-// split-impulse position correction, the object's pre-solve velocities and
+// split-impulse position correction, object 1's pre-solve velocities and
 // pose): they wait in LDS across the solve instead of holding registers.
 constexpr int LDS_STASH_OFFSET = NR * 27;
 constexpr int LDS_STASH_FLOATS = 40;
@@ -437,18 +554,29 @@ constexpr int LDS_FLOATS = LDS_MI_OFFSET + 45;
 constexpr int LDS_FLOATS = LDS_MI_OFFSET;
 #endif
 
-// cube-ground contact: cube-only rows; normal +z, friction dirs of planeSpace(+z) = (0,-1,0), (1,0,0)
+// object-ground contact: object-only rows; normal +z, friction dirs of
+// planeSpace(+z) = (0,-1,0), (1,0,0); wI[j] = I^-1 (r x dir_j) (cylinder only)
 struct GroundContact {
-    V3 r;  // contact point - cube COM
+    V3 r;  // contact point - object COM
     float rhs[3], lam[3], dinv[3];
+    V3 wI[3];
+};
+
+// object-object contact (Stack): A = incident body (+n), B = reference (-n)
+struct PairContact {
+    V3 dir[3], rnA[3], rnB[3];
+    float rhs[3], lam[3], dinv[3];
+    bool a0;  // body A is object 0
 };
 
 // gripper contact: robot rows with explicit Jacobians (M^-1 J^T lives in LDS)
 struct RobotContact {
     float J[3][9];
     V3 dir[3];
-    V3 rn[3];  // cube side: (pB - x_cube) x dir (zero when the contact is with the ground)
+    V3 rn[3];  // object side: (pB - x_obj) x dir (zero when the contact is with the ground)
+    V3 wI[3];  // I^-1 rn (cylinder only)
     float rhs[3], lam[3], dinv[3], mu;
+    bool o1;   // the object is object 1 (Stack)
 };
 
 // per-lane view of the LDS rows: element (slot, row, k) at base[((slot*3 + row)*9 + k) * stride]
@@ -482,6 +610,120 @@ struct Geo {
     V3 ax[9], org[7], spw[PM_NUM_SPHERES];
 };
 
+// row rhs of a contact normal (btSequentialImpulseConstraintSolver setup:
+// speculative margin when separated, ERP/split-impulse when penetrating)
+PS_D float normal_rhs(float dist, float rel, float dinv) {
+    const float dt = (float)PM_TIMESTEP;
+    float pen = dist + (float)PM_LINEAR_SLOP;
+    float velerr = -rel, poserr = 0.0f;
+    if (pen > 0.0f) velerr -= pen / dt;
+    else poserr = -pen * (float)PM_ERP / dt;
+    bool combined = pen > (float)PM_SPLIT_PENETRATION_THRESHOLD;
+    return (combined ? poserr + velerr : velerr) * dinv;
+}
+
+PS_D float safe_inv(float den) { return den > 2.2204460492503131e-16f ? 1.0f / den : 0.0f; }
+
+// Box-box contacts of the two cubes (Stack): the oracle's box_box_contacts
+// (face-axis SAT, incident face clipped against the reference face) in fp32.
+// Fills up to NP contact candidates: point on A (incident), point on B
+// (reference), normal n (B -> A), distance.
+struct PairCand {
+    V3 pA, pB, n;
+    float dist;
+    bool a0;
+};
+
+PS_D int clip_half(const float *iu, const float *iv, const float *id, int n, int axis, float sign, float lim,
+                   float *ou, float *ov, float *od) {
+    int m = 0;
+    for (int i = 0; i < n; i++) {
+        int j = i + 1 == n ? 0 : i + 1;
+        float ca = sign * (axis == 0 ? iu[i] : iv[i]) - lim, cb = sign * (axis == 0 ? iu[j] : iv[j]) - lim;
+        if (ca <= 0.0f) { ou[m] = iu[i]; ov[m] = iv[i]; od[m] = id[i]; m++; }
+        if ((ca < 0.0f && cb > 0.0f) || (ca > 0.0f && cb < 0.0f)) {
+            float t = ca / (ca - cb);
+            ou[m] = iu[i] + t * (iu[j] - iu[i]);
+            ov[m] = iv[i] + t * (iv[j] - iv[i]);
+            od[m] = id[i] + t * (id[j] - id[i]);
+            m++;
+        }
+    }
+    return m;
+}
+
+PS_D int box_box(const Scene &sc, const Body &b0, const Body &b1, const M3 &R0, const M3 &R1, PairCand out[NP]) {
+    const float h[3] = {sc.half.x, sc.half.y, sc.half.z};
+    V3 d = b1.pos - b0.pos;
+    float best = 1e30f;
+    V3 nref = mk(0, 0, 0);
+    int ref = 0, axn = 0;
+    for (int b = 0; b < 2; b++)
+        for (int ax = 0; ax < 3; ax++) {
+            V3 L = col(b == 0 ? R0 : R1, ax);
+            float ra = 0.0f, rb = 0.0f;
+            for (int k = 0; k < 3; k++) {
+                ra += h[k] * fabsf(dot(col(R0, k), L));
+                rb += h[k] * fabsf(dot(col(R1, k), L));
+            }
+            float c = dot(d, L);
+            float pen = ra + rb - fabsf(c);
+            if (pen < -(float)PM_CONTACT_MARGIN_PAIR) return 0;
+            if (pen < best - (float)PM_PAIR_AXIS_TOL) {
+                best = pen;
+                ref = b;
+                axn = ax;
+                float sg = (b == 0 ? c : -c) >= 0.0f ? 1.0f : -1.0f;
+                nref = L * sg;
+            }
+        }
+    const M3 &Rr = ref == 0 ? R0 : R1;
+    const M3 &Ri = ref == 0 ? R1 : R0;
+    V3 cr = ref == 0 ? b0.pos : b1.pos, ci = ref == 0 ? b1.pos : b0.pos;
+    int a1 = axn + 1 == 3 ? 0 : axn + 1, a2 = axn + 2 >= 3 ? axn - 1 : axn + 2;
+    V3 t1 = col(Rr, a1), t2 = col(Rr, a2);
+    V3 cf = cr + nref * h[axn];
+    int ai = 0;
+    float mostneg = 2.0f, si = 1.0f;
+    for (int ax = 0; ax < 3; ax++) {
+        float dn = dot(col(Ri, ax), nref);
+        if (-fabsf(dn) < mostneg) { mostneg = -fabsf(dn); ai = ax; si = dn > 0.0f ? -1.0f : 1.0f; }
+    }
+    int b1i = ai + 1 == 3 ? 0 : ai + 1, b2i = ai + 2 >= 3 ? ai - 1 : ai + 2;
+    float pu[16], pv[16], pd[16], tu[16], tv[16], td[16];
+    const float cu[4] = {-1, 1, 1, -1}, cv[4] = {-1, -1, 1, 1};
+    for (int k = 0; k < 4; k++) {
+        float loc[3];
+        loc[ai] = si * h[ai];
+        loc[b1i] = cu[k] * h[b1i];
+        loc[b2i] = cv[k] * h[b2i];
+        V3 rel = mul(Ri, mk(loc[0], loc[1], loc[2])) + ci - cf;
+        pu[k] = dot(rel, t1);
+        pv[k] = dot(rel, t2);
+        pd[k] = dot(rel, nref);
+    }
+    int n = 4;
+    n = clip_half(pu, pv, pd, n, 0, 1.0f, h[a1], tu, tv, td);
+    n = clip_half(tu, tv, td, n, 0, -1.0f, h[a1], pu, pv, pd);
+    n = clip_half(pu, pv, pd, n, 1, 1.0f, h[a2], tu, tv, td);
+    n = clip_half(tu, tv, td, n, 1, -1.0f, h[a2], pu, pv, pd);
+    int m = 0;
+    for (int k = 0; k < n; k++)
+        if (pd[k] < (float)PM_CONTACT_MARGIN_PAIR) { tu[m] = pu[k]; tv[m] = pv[k]; td[m] = pd[k]; m++; }
+    int take = m < NP ? m : NP;
+    for (int k = 0; k < take; k++) {
+        int idx = m <= NP ? k : (k * m) / NP;
+        PairCand c;
+        c.pB = cf + t1 * tu[idx] + t2 * tv[idx];
+        c.pA = c.pB + nref * td[idx];
+        c.n = nref;
+        c.dist = td[idx];
+        c.a0 = ref == 1;  // A = incident
+        out[k] = c;
+    }
+    return take;
+}
+
 // ----------------------------------------------------------------- substep
 // One btMultiBodyDynamicsWorld::stepSimulation(1/500 s): see the oracle's
 // po_substep for the row-by-row restatement this mirrors.
@@ -493,8 +735,13 @@ PS_D float res_scale(float dinv) { return __builtin_amdgcn_rcpf(dinv); }
 // STD_MOTORS: the motors are the ones RobotTaskEnv.step sets (POSITION_CONTROL
 // on all nine joints with the fixed Panda gains and forces, panda.py:40-56), so
 // only the targets are per-env; otherwise every gain comes from `mt`.
-template <bool HAS_CUBE, bool STD_MOTORS>
-PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cube &cb, const MJStore &lds PS_PROF_PARAM) {
+template <int NOBJ, int SHAPE, bool STD_MOTORS>
+PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Body *bd, const MJStore &lds
+                  PS_PROF_PARAM) {
+    static_assert(NOBJ >= 0 && NOBJ <= 2, "objects");
+    static_assert(NOBJ < 2 || SHAPE == SHAPE_BOX, "Stack stacks cubes");
+    constexpr int NB = NOBJ > 0 ? NOBJ : 1;  // array extents
+    constexpr bool ANISO = SHAPE == SHAPE_CYL;
     const float dt = (float)PM_TIMESTEP;
     float Mi[45], hb[9];
     Geo geo;
@@ -544,17 +791,28 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
         for (int b = 0; b < 9; b++) s -= Mi[sidx(a, b)] * hb[b];
         v1[a] = qd[a] + dt * s;
     }
-    // cube: gravity + btMultiBody damping (isotropic inertia: no gyroscopic term)
-    V3 cw1 = mk(0, 0, 0), cv1 = mk(0, 0, 0);
-    float inv_I = 0.0f, inv_m = 0.0f;
-    if constexpr (HAS_CUBE) {
-        float l = 2.0f * sc.half;
-        inv_I = 1.0f / (sc.mass / 12.0f * (2.0f * l * l));
-        inv_m = 1.0f / sc.mass;
-        float cl = (float)PM_LINEAR_DAMPING + (float)PM_LINEAR_DAMPING * norm(cb.vel);
-        float ca = (float)PM_ANGULAR_DAMPING + (float)PM_ANGULAR_DAMPING * norm(cb.omg);
-        cv1 = cb.vel + (mk(0, 0, (float)PM_GRAVITY_Z) - cb.vel * cl) * dt;
-        cw1 = cb.omg - cb.omg * (ca * dt);
+    // objects: gravity + btMultiBody base damping, plus the gyroscopic torque
+    // -w x (I w) for the (anisotropic) cylinder
+    V3 cw1[NB], cv1[NB];
+    BodyDyn<SHAPE> od[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        cw1[b] = mk(0, 0, 0);
+        cv1[b] = mk(0, 0, 0);
+    }
+#pragma unroll
+    for (int b = 0; b < NOBJ; b++) {
+        od[b] = body_dyn<SHAPE>(sc, bd[b], b == 0 ? sc.mass : sc.mass2);
+        float cl = (float)PM_LINEAR_DAMPING + (float)PM_LINEAR_DAMPING * norm(bd[b].vel);
+        float ca = (float)PM_ANGULAR_DAMPING + (float)PM_ANGULAR_DAMPING * norm(bd[b].omg);
+        cv1[b] = bd[b].vel + (mk(0, 0, (float)PM_GRAVITY_Z) - bd[b].vel * cl) * dt;
+        cw1[b] = bd[b].omg - bd[b].omg * (ca * dt);
+        if constexpr (ANISO) {
+            V3 I = local_inertia<SHAPE>(sc, b == 0 ? sc.mass : sc.mass2);
+            S3 Iw = rotate_diag(od[b].R, I.x, I.y, I.z);
+            V3 gyro = od[b].inv_inertia(cross(bd[b].omg, mul(Iw, bd[b].omg)));
+            cw1[b] = cw1[b] - gyro * dt;
+        }
     }
 
     // ---- joint-space rows: limits and motors.  A joint can be beyond at most
@@ -595,26 +853,28 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
         mot_lam[d] = 0.0f;
     }
 
-    // ---- contacts
-    GroundContact gc[NG];
+    // ---- contacts (oracle gen_contacts order: ground per object, pairs, gripper)
+    GroundContact gc[NB][NG];
+    int ng[NB];
 #pragma unroll
-    for (int s = 0; s < NG; s++) gc[s] = GroundContact{mk(0, 0, 0), {0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
-    int ng = 0;
-    RobotContact rc[NR];
-    int nr = 0;
-    M3 Rc;
-    if constexpr (HAS_CUBE) {
-        Rc = quat_to_mat(cb.quat);
-        const float h = sc.half;
+    for (int b = 0; b < NB; b++) {
+        ng[b] = 0;
 #pragma unroll
-        for (int v = 0; v < 8; v++) {
-            V3 loc = mk((v & 1) ? h : -h, (v & 2) ? h : -h, (v & 4) ? h : -h);
-            V3 pw = cb.pos + mul(Rc, loc);
+        for (int s = 0; s < NG; s++)
+            gc[b][s] = GroundContact{mk(0, 0, 0), {0, 0, 0}, {0, 0, 0}, {0, 0, 0},
+                                     {mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 0)}};
+    }
+    const float gmu = sc.fric * (float)PM_DEFAULT_FRICTION;
+#pragma unroll
+    for (int b = 0; b < NOBJ; b++) {
+        static_for<0, num_support<SHAPE>()>([&](auto VV) {
+            constexpr int V = decltype(VV)::value;
+            V3 pw = bd[b].pos + mul(od[b].R, support_point<SHAPE, V>(sc));
             float top;
-            if (ng < NG && ground_top(sc, pw.x, pw.y, top)) {
+            if (ng[b] < NG && ground_top(sc, pw.x, pw.y, top)) {
                 float dist = pw.z - top;
                 if (dist < (float)PM_CONTACT_MARGIN_GROUND) {
-                    V3 r = pw - cb.pos;
+                    V3 r = pw - bd[b].pos;
                     // normal (0,0,1), t1 (0,-1,0), t2 (1,0,0)
                     V3 dirs[3] = {mk(0, 0, 1), mk(0, -1, 0), mk(1, 0, 0)};
                     GroundContact g;
@@ -622,42 +882,82 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
 #pragma unroll
                     for (int j = 0; j < 3; j++) {
                         V3 rn = cross(r, dirs[j]);
-                        float den = dot(rn, rn) * inv_I + dot(dirs[j], dirs[j]) * inv_m;
-                        g.dinv[j] = den > 2.2204460492503131e-16f ? 1.0f / den : 0.0f;
-                        float rel = dot(rn, cw1) + dot(dirs[j], cv1);
+                        V3 w = od[b].inv_inertia(rn);
+                        if constexpr (ANISO) g.wI[j] = w;
+                        float den = dot(rn, w) + dot(dirs[j], dirs[j]) * od[b].inv_m;
+                        g.dinv[j] = safe_inv(den);
+                        float rel = dot(rn, cw1[b]) + dot(dirs[j], cv1[b]);
                         g.lam[j] = 0.0f;
-                        if (j == 0) {
-                            float pen = dist + (float)PM_LINEAR_SLOP;
-                            float velerr = -rel, poserr = 0.0f;
-                            if (pen > 0.0f) velerr -= pen / dt;
-                            else poserr = -pen * (float)PM_ERP / dt;
-                            bool combined = pen > (float)PM_SPLIT_PENETRATION_THRESHOLD;
-                            g.rhs[0] = (combined ? poserr + velerr : velerr) * g.dinv[0];
-                        } else {
-                            g.rhs[j] = -rel * g.dinv[j];
-                        }
+                        g.rhs[j] = j == 0 ? normal_rhs(dist, rel, g.dinv[0]) : -rel * g.dinv[j];
                     }
 #pragma unroll
                     for (int s = 0; s < NG; s++)
-                        if (s == ng) gc[s] = g;
-                    ng++;
+                        if (s == ng[b]) gc[b][s] = g;
+                    ng[b]++;
+                }
+            }
+        });
+    }
+    PairContact pc[NP];
+    int np = 0;
+    if constexpr (NOBJ == 2) {
+        PairCand cand[NP];
+        np = box_box(sc, bd[0], bd[1], od[0].R, od[1].R, cand);
+        const float pmu = sc.fric * sc.fric;
+        (void)pmu;
+#pragma unroll
+        for (int c = 0; c < NP; c++) {
+            PairContact &p = pc[c];
+            if (c < np) {
+                const PairCand &cd = cand[c];
+                int A = cd.a0 ? 0 : 1;
+                V3 dirs[3];
+                dirs[0] = cd.n;
+                plane_space(cd.n, dirs[1], dirs[2]);
+                V3 rA = cd.pA - (A == 0 ? bd[0].pos : bd[1].pos), rB = cd.pB - (A == 0 ? bd[1].pos : bd[0].pos);
+                p.a0 = cd.a0;
+#pragma unroll
+                for (int j = 0; j < 3; j++) {
+                    V3 dj = dirs[j];
+                    p.dir[j] = dj;
+                    p.rnA[j] = cross(rA, dj);
+                    p.rnB[j] = cross(rB, dj);
+                    float iIA = A == 0 ? od[0].iI : od[1].iI, iIB = A == 0 ? od[1].iI : od[0].iI;
+                    float imA = A == 0 ? od[0].inv_m : od[1].inv_m, imB = A == 0 ? od[1].inv_m : od[0].inv_m;
+                    float den = dot(p.rnA[j], p.rnA[j]) * iIA + dot(p.rnB[j], p.rnB[j]) * iIB + dot(dj, dj) * (imA + imB);
+                    p.dinv[j] = safe_inv(den);
+                    V3 wA = A == 0 ? cw1[0] : cw1[1], vA = A == 0 ? cv1[0] : cv1[1];
+                    V3 wB = A == 0 ? cw1[1] : cw1[0], vB = A == 0 ? cv1[1] : cv1[0];
+                    float rel = dot(p.rnA[j], wA) + dot(dj, vA) - dot(p.rnB[j], wB) - dot(dj, vB);
+                    p.lam[j] = 0.0f;
+                    p.rhs[j] = j == 0 ? normal_rhs(cd.dist, rel, p.dinv[0]) : -rel * p.dinv[j];
+                }
+            } else {
+                p.a0 = true;
+#pragma unroll
+                for (int j = 0; j < 3; j++) {
+                    p.dir[j] = p.rnA[j] = p.rnB[j] = mk(0, 0, 0);
+                    p.rhs[j] = p.lam[j] = p.dinv[j] = 0.0f;
                 }
             }
         }
     }
+    RobotContact rc[NR];
+    int nr = 0;
     {
-        // 1) candidate gripper contacts in spec order (spheres vs cube, then
-        //    spheres vs ground) -> small records; the first NR active ones
-        //    are assigned slots 0..NR-1 (select into compile-time slots)
+        // 1) candidate gripper contacts in spec order (spheres vs object 1,
+        //    vs object 2, then spheres vs ground) -> small records; the first
+        //    NR active ones are assigned slots 0..NR-1 (select into
+        //    compile-time slots)
         struct Cand {
             V3 pA, pB, n;
             float dist, mu;
             int link;
-            bool on_cube;
+            int obj;  // -1: ground
         };
         Cand slot[NR];
 #pragma unroll
-        for (int s = 0; s < NR; s++) slot[s] = Cand{mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 1), 1.0f, 0.0f, 8, false};
+        for (int s = 0; s < NR; s++) slot[s] = Cand{mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 1), 1.0f, 0.0f, 8, -1};
         auto offer = [&](const Cand &c) {
 #pragma unroll
             for (int s = 0; s < NR; s++)
@@ -665,36 +965,18 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
             nr++;
         };
 #ifndef PS_DBG_NO_RC
-        if constexpr (HAS_CUBE) {
-            const float h = sc.half;
+#pragma unroll
+        for (int b = 0; b < NOBJ; b++) {
             static_for<0, PM_NUM_SPHERES>([&](auto SS) {
                 constexpr int S = decltype(SS)::value;
                 constexpr SphereDef s = sphere_def(S);
-                V3 loc = tmul(Rc, geo.spw[S] - cb.pos);
-                V3 cl = mk(fminf(fmaxf(loc.x, -h), h), fminf(fmaxf(loc.y, -h), h), fminf(fmaxf(loc.z, -h), h));
-                V3 dif = loc - cl;
-                float dn = norm(dif);
-                V3 nl;
-                float dist;
-                if (dn > 1e-9f) {
-                    nl = dif * (1.0f / dn);
-                    dist = dn - (float)s.r;
-                } else {
-                    float bx = h - fabsf(loc.x), by = h - fabsf(loc.y), bz = h - fabsf(loc.z);
-                    int ax = 0;
-                    float best = bx;
-                    if (by < best) { best = by; ax = 1; }
-                    if (bz < best) { best = bz; ax = 2; }
-                    float sg;
-                    if (ax == 0) { sg = loc.x >= 0.0f ? 1.0f : -1.0f; nl = mk(sg, 0, 0); cl.x = sg * h; }
-                    else if (ax == 1) { sg = loc.y >= 0.0f ? 1.0f : -1.0f; nl = mk(0, sg, 0); cl.y = sg * h; }
-                    else { sg = loc.z >= 0.0f ? 1.0f : -1.0f; nl = mk(0, 0, sg); cl.z = sg * h; }
-                    dist = -best - (float)s.r;
-                }
+                V3 loc = tmul(od[b].R, geo.spw[S] - bd[b].pos);
+                V3 cl, nl;
+                float dist = object_closest<SHAPE>(sc, loc, cl, nl) - (float)s.r;
                 if (nr < NR && dist < (float)PM_CONTACT_MARGIN_SPHERE) {
-                    V3 n = mul(Rc, nl);
-                    offer(Cand{geo.spw[S] - n * (float)s.r, cb.pos + mul(Rc, cl), n, dist,
-                               (float)(s.mu * PM_DEFAULT_FRICTION), s.link, true});
+                    V3 n = mul(od[b].R, nl);
+                    offer(Cand{geo.spw[S] - n * (float)s.r, bd[b].pos + mul(od[b].R, cl), n, dist,
+                               (float)s.mu * sc.fric, s.link, b});
                 }
             });
         }
@@ -706,7 +988,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
                 float dist = geo.spw[S].z - (float)s.r - top;
                 if (dist < (float)PM_CONTACT_MARGIN_SPHERE) {
                     V3 pA = geo.spw[S] - mk(0, 0, (float)s.r);
-                    offer(Cand{pA, pA, mk(0, 0, 1), dist, (float)(s.mu * PM_DEFAULT_FRICTION), s.link, false});
+                    offer(Cand{pA, pA, mk(0, 0, 1), dist, (float)(s.mu * PM_DEFAULT_FRICTION), s.link, -1});
                 }
             }
         });
@@ -714,15 +996,21 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
         // 2) rows of each used slot: J (registers), M^-1 J^T (LDS), rhs, bounds
 #pragma unroll
         for (int sl = 0; sl < NR; sl++) {
+            RobotContact &c = rc[sl];
             if (sl < nr) {
                 const Cand &cd = slot[sl];
-                RobotContact &c = rc[sl];
                 V3 dirs[3];
                 dirs[0] = cd.n;
                 plane_space(cd.n, dirs[1], dirs[2]);
                 c.mu = cd.mu;
+                c.o1 = cd.obj == 1;
+                bool on_obj = NOBJ > 0 && cd.obj >= 0;
                 V3 p = cd.pA - sc.base;
-                V3 rB = cd.pB - cb.pos;
+                V3 opos = NOBJ == 2 && cd.obj == 1 ? bd[NB - 1].pos : bd[0].pos;
+                V3 rB = cd.pB - opos;
+                V3 ow = NOBJ == 2 && cd.obj == 1 ? cw1[NB - 1] : cw1[0];
+                V3 ov = NOBJ == 2 && cd.obj == 1 ? cv1[NB - 1] : cv1[0];
+                float oim = NOBJ == 2 && cd.obj == 1 ? od[NB - 1].inv_m : od[0].inv_m;
 #pragma unroll
                 for (int j = 0; j < 3; j++) {
                     V3 dj = dirs[j];
@@ -740,29 +1028,25 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
                         den += c.J[j][a] * s;
                     }
                     float rel = jrow_dot(c.J[j], v1);
-                    c.rn[j] = cd.on_cube ? cross(rB, dj) : mk(0, 0, 0);
-                    c.dir[j] = cd.on_cube ? dj : mk(0, 0, 0);  // cube side only
-                    if (cd.on_cube) {
-                        den += dot(c.rn[j], c.rn[j]) * inv_I + dot(dj, dj) * inv_m;
-                        rel -= dot(c.rn[j], cw1) + dot(dj, cv1);
+                    c.rn[j] = on_obj ? cross(rB, dj) : mk(0, 0, 0);
+                    c.dir[j] = on_obj ? dj : mk(0, 0, 0);  // object side only
+                    if constexpr (NOBJ > 0) {
+                        V3 w = ANISO ? od[0].inv_inertia(c.rn[j])
+                                     : c.rn[j] * (NOBJ == 2 && cd.obj == 1 ? od[NB - 1].iI : od[0].iI);
+                        if constexpr (ANISO) c.wI[j] = w;
+                        if (on_obj) {
+                            den += dot(c.rn[j], w) + dot(dj, dj) * oim;
+                            rel -= dot(c.rn[j], ow) + dot(dj, ov);
+                        }
                     }
-                    c.dinv[j] = den > 2.2204460492503131e-16f ? 1.0f / den : 0.0f;
+                    c.dinv[j] = safe_inv(den);
                     c.lam[j] = 0.0f;
-                    if (j == 0) {
-                        float pen = cd.dist + (float)PM_LINEAR_SLOP;
-                        float velerr = -rel, poserr = 0.0f;
-                        if (pen > 0.0f) velerr -= pen / dt;
-                        else poserr = -pen * (float)PM_ERP / dt;
-                        bool combined = pen > (float)PM_SPLIT_PENETRATION_THRESHOLD;
-                        c.rhs[0] = (combined ? poserr + velerr : velerr) * c.dinv[0];
-                    } else {
-                        c.rhs[j] = -rel * c.dinv[j];
-                    }
+                    c.rhs[j] = j == 0 ? normal_rhs(cd.dist, rel, c.dinv[0]) : -rel * c.dinv[j];
                 }
             } else {
                 // unused slot: all-zero rows (finite M^-1 J^T too) are no-ops in PGS
-                RobotContact &c = rc[sl];
                 c.mu = 0.0f;
+                c.o1 = false;
 #pragma unroll
                 for (int j = 0; j < 3; j++) {
 #pragma unroll
@@ -770,8 +1054,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
                         c.J[j][a] = 0.0f;
                         lds.at(sl, j, a) = 0.0f;
                     }
-                    c.dir[j] = mk(0, 0, 0);
-                    c.rn[j] = mk(0, 0, 0);
+                    c.dir[j] = c.rn[j] = c.wI[j] = mk(0, 0, 0);
                     c.rhs[j] = c.lam[j] = c.dinv[j] = 0.0f;
                 }
             }
@@ -785,11 +1068,12 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
         lds.stash(9 + d) = v1[d];
         lds.stash(18 + d) = split_dq[d];
     }
-    if constexpr (HAS_CUBE) {
-        lds.stash(27) = cw1.x; lds.stash(28) = cw1.y; lds.stash(29) = cw1.z;
-        lds.stash(30) = cv1.x; lds.stash(31) = cv1.y; lds.stash(32) = cv1.z;
-        lds.stash(33) = cb.pos.x; lds.stash(34) = cb.pos.y; lds.stash(35) = cb.pos.z;
-        lds.stash(36) = cb.quat.x; lds.stash(37) = cb.quat.y; lds.stash(38) = cb.quat.z; lds.stash(39) = cb.quat.w;
+    if constexpr (NOBJ > 0) {
+        lds.stash(27) = cw1[0].x; lds.stash(28) = cw1[0].y; lds.stash(29) = cw1[0].z;
+        lds.stash(30) = cv1[0].x; lds.stash(31) = cv1[0].y; lds.stash(32) = cv1[0].z;
+        lds.stash(33) = bd[0].pos.x; lds.stash(34) = bd[0].pos.y; lds.stash(35) = bd[0].pos.z;
+        lds.stash(36) = bd[0].quat.x; lds.stash(37) = bd[0].quat.y; lds.stash(38) = bd[0].quat.z;
+        lds.stash(39) = bd[0].quat.w;
     }
 
     // ---- projected Gauss-Seidel
@@ -800,7 +1084,12 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
     float dv[9];
 #pragma unroll
     for (int d = 0; d < 9; d++) dv[d] = 0.0f;
-    V3 dw = mk(0, 0, 0), dvl = mk(0, 0, 0);
+    V3 dw[NB], dvl[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+        dw[b] = mk(0, 0, 0);
+        dvl[b] = mk(0, 0, 0);
+    }
     float res;
     MJStore L = lds;
 
@@ -818,7 +1107,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
             for (int a = 0; a < 9; a++) dv[a] += L.mi(sidx(a, d)) * f;
         }
         float x = dl * (MI_REGS ? Mi[sidx(d, d)] : (float)L.mi(sidx(d, d)));  // residual dl / dinv
-        res = fmaxf(res, x * x);
+        res = fmaxf(res, fabsf(x));
     };
     auto limit_row = [&](int d) {
         if (__builtin_amdgcn_ballot_w64((lim_on >> d) & 1u)) {
@@ -831,23 +1120,64 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
         float imp = STD_MOTORS ? (float)(joint_force(d) * PM_TIMESTEP) : mt.imp[d];
         joint_row(d, 1.0f, mot_rhs[d], mot_lam[d], -imp, imp);
     };
+    // body-side velocity change of object `o1 ? 1 : 0` (Stack selects; the
+    // other scenes have one object and the select folds away)
+    auto obj_add = [&](bool o1, V3 ddw, V3 ddv) {
+        if constexpr (NOBJ == 2) {
+            dw[0] = dw[0] + (o1 ? mk(0, 0, 0) : ddw);
+            dvl[0] = dvl[0] + (o1 ? mk(0, 0, 0) : ddv);
+            dw[NB - 1] = dw[NB - 1] + (o1 ? ddw : mk(0, 0, 0));
+            dvl[NB - 1] = dvl[NB - 1] + (o1 ? ddv : mk(0, 0, 0));
+        } else {
+            dw[0] = dw[0] + ddw;
+            dvl[0] = dvl[0] + ddv;
+        }
+    };
+    auto obj_dw = [&](bool o1) { return NOBJ == 2 && o1 ? dw[NB - 1] : dw[0]; };
+    auto obj_dv = [&](bool o1) { return NOBJ == 2 && o1 ? dvl[NB - 1] : dvl[0]; };
 
     auto contacts = [&]() {
-        // normals: ground contacts then gripper contacts
-        if constexpr (HAS_CUBE) {
+        // normals: ground contacts, pair contacts, then gripper contacts
+#pragma unroll
+        for (int b = 0; b < NOBJ; b++) {
+            const float inv_m = od[b].inv_m;
 #pragma unroll
             for (int c = 0; c < NG; c++)
-                if (__builtin_amdgcn_ballot_w64(c < ng)) {
-                    GroundContact &g = gc[c];
+                if (__builtin_amdgcn_ballot_w64(c < ng[b])) {
+                    GroundContact &g = gc[b][c];
                     V3 rn = mk(g.r.y, -g.r.x, 0.0f);  // r x (0,0,1)
-                    float dl = g.rhs[0] - g.dinv[0] * (dot(rn, dw) + dvl.z);
+                    float dl = g.rhs[0] - g.dinv[0] * (dot(rn, dw[b]) + dvl[b].z);
                     float nl = fminf(fmaxf(g.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
                     dl = nl - g.lam[0];
                     g.lam[0] = nl;
-                    dw = dw + rn * (dl * inv_I);
-                    dvl.z += dl * inv_m;
-                    float x = dl * res_scale(g.dinv[0]);
-                    res = fmaxf(res, x * x);
+                    if constexpr (ANISO) {
+                        dw[b] = mk(fmaf(g.wI[0].x, dl, dw[b].x), fmaf(g.wI[0].y, dl, dw[b].y), fmaf(g.wI[0].z, dl, dw[b].z));
+                    } else {
+                        float dI = dl * od[b].iI;
+                        dw[b].x = fmaf(rn.x, dI, dw[b].x);
+                        dw[b].y = fmaf(rn.y, dI, dw[b].y);
+                    }
+                    dvl[b].z = fmaf(dl, inv_m, dvl[b].z);
+                    res = fmaxf(res, fabsf(dl * res_scale(g.dinv[0])));
+                }
+        }
+        if constexpr (NOBJ == 2) {
+#pragma unroll
+            for (int c = 0; c < NP; c++)
+                if (__builtin_amdgcn_ballot_w64(c < np)) {
+                    PairContact &p = pc[c];
+                    bool A1 = !p.a0;
+                    V3 wA = obj_dw(A1), vA = obj_dv(A1), wB = obj_dw(!A1), vB = obj_dv(!A1);
+                    float jv = dot(p.rnA[0], wA) + dot(p.dir[0], vA) - dot(p.rnB[0], wB) - dot(p.dir[0], vB);
+                    float dl = p.rhs[0] - p.dinv[0] * jv;
+                    float nl = fminf(fmaxf(p.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
+                    dl = nl - p.lam[0];
+                    p.lam[0] = nl;
+                    float iIA = A1 ? od[NB - 1].iI : od[0].iI, iIB = A1 ? od[0].iI : od[NB - 1].iI;
+                    float imA = A1 ? od[NB - 1].inv_m : od[0].inv_m, imB = A1 ? od[0].inv_m : od[NB - 1].inv_m;
+                    obj_add(A1, p.rnA[0] * (dl * iIA), p.dir[0] * (dl * imA));
+                    obj_add(!A1, p.rnB[0] * (-dl * iIB), p.dir[0] * (-dl * imB));
+                    res = fmaxf(res, fabsf(dl * res_scale(p.dinv[0])));
                 }
         }
 #pragma unroll
@@ -855,32 +1185,34 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
             if (__builtin_amdgcn_ballot_w64(c < nr)) {
                 RobotContact &r = rc[c];
                 float jv = jrow_dot(r.J[0], dv);
-                if (HAS_CUBE) jv -= dot(r.rn[0], dw) + dot(r.dir[0], dvl);
+                if (NOBJ > 0) jv -= dot(r.rn[0], obj_dw(r.o1)) + dot(r.dir[0], obj_dv(r.o1));
                 float dl = r.rhs[0] - r.dinv[0] * jv;
                 float nl = fminf(fmaxf(r.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
                 dl = nl - r.lam[0];
                 r.lam[0] = nl;
 #pragma unroll
-                for (int a = 0; a < 9; a++) dv[a] += L.at(c, 0, a) * dl;
-                if (HAS_CUBE) {
-                    dw = dw - r.rn[0] * (dl * inv_I);
-                    dvl = dvl - r.dir[0] * (dl * inv_m);
+                for (int a = 0; a < 9; a++) dv[a] = fmaf(L.at(c, 0, a), dl, dv[a]);
+                if constexpr (NOBJ > 0) {
+                    float im = NOBJ == 2 && r.o1 ? od[NB - 1].inv_m : od[0].inv_m;
+                    float iI = NOBJ == 2 && r.o1 ? od[NB - 1].iI : od[0].iI;
+                    obj_add(r.o1, ANISO ? r.wI[0] * -dl : r.rn[0] * (-dl * iI), r.dir[0] * (-dl * im));
                 }
-                float x = dl * res_scale(r.dinv[0]);
-                res = fmaxf(res, x * x);
+                res = fmaxf(res, fabsf(dl * res_scale(r.dinv[0])));
             }
         // friction cones
-        if constexpr (HAS_CUBE) {
+#pragma unroll
+        for (int b = 0; b < NOBJ; b++) {
+            const float inv_m = od[b].inv_m;
 #pragma unroll
             for (int c = 0; c < NG; c++)
-                if (__builtin_amdgcn_ballot_w64(c < ng)) {
-                    GroundContact &g = gc[c];
+                if (__builtin_amdgcn_ballot_w64(c < ng[b])) {
+                    GroundContact &g = gc[b][c];
                     V3 r1 = mk(g.r.z, 0.0f, -g.r.x);  // r x (0,-1,0)
                     V3 r2 = mk(0.0f, g.r.z, -g.r.y);  // r x (1,0,0)
-                    float dla = g.rhs[1] - g.dinv[1] * (dot(r1, dw) - dvl.y);
-                    float dlb = g.rhs[2] - g.dinv[2] * (dot(r2, dw) + dvl.x);
+                    float dla = g.rhs[1] - g.dinv[1] * (dot(r1, dw[b]) - dvl[b].y);
+                    float dlb = g.rhs[2] - g.dinv[2] * (dot(r2, dw[b]) + dvl[b].x);
                     float sa = g.lam[1] + dla, sb = g.lam[2] + dlb;
-                    float lim = (float)(PM_DEFAULT_FRICTION * PM_DEFAULT_FRICTION) * fmaxf(g.lam[0], 0.0f);
+                    float lim = gmu * fmaxf(g.lam[0], 0.0f);
                     float m2 = sa * sa + sb * sb;
                     // |f| > mu N: project onto the cone (lim * rsq(m2) <= 1 there)
                     float s = m2 > lim * lim ? lim * rsqrtf(m2) : 1.0f;
@@ -890,11 +1222,47 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
                     dlb = sb - g.lam[2];
                     g.lam[1] = sa;
                     g.lam[2] = sb;
-                    dw = dw + (r1 * dla + r2 * dlb) * inv_I;
-                    dvl = dvl + mk(dlb, -dla, 0.0f) * inv_m;
-                    float ra = dla * res_scale(g.dinv[1]), rb = dlb * res_scale(g.dinv[2]);
-                    float x = fabsf(ra) > fabsf(rb) ? ra : rb;
-                    res = fmaxf(res, x * x);
+                    if constexpr (ANISO) {
+                        dw[b] = mk(fmaf(g.wI[2].x, dlb, fmaf(g.wI[1].x, dla, dw[b].x)),
+                                   fmaf(g.wI[2].y, dlb, fmaf(g.wI[1].y, dla, dw[b].y)),
+                                   fmaf(g.wI[2].z, dlb, fmaf(g.wI[1].z, dla, dw[b].z)));
+                    } else {
+                        float aI = dla * od[b].iI, bI = dlb * od[b].iI;
+                        dw[b].x = fmaf(r1.x, aI, dw[b].x);
+                        dw[b].y = fmaf(r2.y, bI, dw[b].y);
+                        dw[b].z = fmaf(r2.z, bI, fmaf(r1.z, aI, dw[b].z));
+                    }
+                    dvl[b].x = fmaf(dlb, inv_m, dvl[b].x);
+                    dvl[b].y = fmaf(-dla, inv_m, dvl[b].y);
+                    res = fmaxf(res, fmaxf(fabsf(dla * res_scale(g.dinv[1])), fabsf(dlb * res_scale(g.dinv[2]))));
+                }
+        }
+        if constexpr (NOBJ == 2) {
+            const float pmu = sc.fric * sc.fric;
+#pragma unroll
+            for (int c = 0; c < NP; c++)
+                if (__builtin_amdgcn_ballot_w64(c < np)) {
+                    PairContact &p = pc[c];
+                    bool A1 = !p.a0;
+                    V3 wA = obj_dw(A1), vA = obj_dv(A1), wB = obj_dw(!A1), vB = obj_dv(!A1);
+                    float ja = dot(p.rnA[1], wA) + dot(p.dir[1], vA) - dot(p.rnB[1], wB) - dot(p.dir[1], vB);
+                    float jb = dot(p.rnA[2], wA) + dot(p.dir[2], vA) - dot(p.rnB[2], wB) - dot(p.dir[2], vB);
+                    float dla = p.rhs[1] - p.dinv[1] * ja, dlb = p.rhs[2] - p.dinv[2] * jb;
+                    float sa = p.lam[1] + dla, sb = p.lam[2] + dlb;
+                    float lim = pmu * fmaxf(p.lam[0], 0.0f);
+                    float m2 = sa * sa + sb * sb;
+                    float s = m2 > lim * lim ? lim * rsqrtf(m2) : 1.0f;
+                    sa *= s;
+                    sb *= s;
+                    dla = sa - p.lam[1];
+                    dlb = sb - p.lam[2];
+                    p.lam[1] = sa;
+                    p.lam[2] = sb;
+                    float iIA = A1 ? od[NB - 1].iI : od[0].iI, iIB = A1 ? od[0].iI : od[NB - 1].iI;
+                    float imA = A1 ? od[NB - 1].inv_m : od[0].inv_m, imB = A1 ? od[0].inv_m : od[NB - 1].inv_m;
+                    obj_add(A1, (p.rnA[1] * dla + p.rnA[2] * dlb) * iIA, (p.dir[1] * dla + p.dir[2] * dlb) * imA);
+                    obj_add(!A1, (p.rnB[1] * dla + p.rnB[2] * dlb) * -iIB, (p.dir[1] * dla + p.dir[2] * dlb) * -imB);
+                    res = fmaxf(res, fmaxf(fabsf(dla * res_scale(p.dinv[1])), fabsf(dlb * res_scale(p.dinv[2]))));
                 }
         }
 #pragma unroll
@@ -902,9 +1270,10 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
             if (__builtin_amdgcn_ballot_w64(c < nr)) {
                 RobotContact &r = rc[c];
                 float ja = jrow_dot(r.J[1], dv), jb = jrow_dot(r.J[2], dv);
-                if (HAS_CUBE) {
-                    ja -= dot(r.rn[1], dw) + dot(r.dir[1], dvl);
-                    jb -= dot(r.rn[2], dw) + dot(r.dir[2], dvl);
+                if (NOBJ > 0) {
+                    V3 ow = obj_dw(r.o1), ov = obj_dv(r.o1);
+                    ja -= dot(r.rn[1], ow) + dot(r.dir[1], ov);
+                    jb -= dot(r.rn[2], ow) + dot(r.dir[2], ov);
                 }
                 float dla = r.rhs[1] - r.dinv[1] * ja, dlb = r.rhs[2] - r.dinv[2] * jb;
                 float sa = r.lam[1] + dla, sb = r.lam[2] + dlb;
@@ -918,14 +1287,25 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
                 r.lam[1] = sa;
                 r.lam[2] = sb;
 #pragma unroll
-                for (int a = 0; a < 9; a++) dv[a] += L.at(c, 1, a) * dla + L.at(c, 2, a) * dlb;
-                if (HAS_CUBE) {
-                    dw = dw - (r.rn[1] * dla + r.rn[2] * dlb) * inv_I;
-                    dvl = dvl - (r.dir[1] * dla + r.dir[2] * dlb) * inv_m;
+                for (int a = 0; a < 9; a++) dv[a] = fmaf(L.at(c, 2, a), dlb, fmaf(L.at(c, 1, a), dla, dv[a]));
+                if constexpr (NOBJ > 0) {
+                    float im = NOBJ == 2 && r.o1 ? od[NB - 1].inv_m : od[0].inv_m;
+                    V3 ddw;
+                    if constexpr (ANISO) {
+                        ddw = mk(fmaf(r.wI[2].x, -dlb, -dla * r.wI[1].x), fmaf(r.wI[2].y, -dlb, -dla * r.wI[1].y),
+                                 fmaf(r.wI[2].z, -dlb, -dla * r.wI[1].z));
+                    } else {
+                        float iI = NOBJ == 2 && r.o1 ? od[NB - 1].iI : od[0].iI;
+                        float aI = -dla * iI, bI = -dlb * iI;
+                        ddw = mk(fmaf(r.rn[2].x, bI, r.rn[1].x * aI), fmaf(r.rn[2].y, bI, r.rn[1].y * aI),
+                                 fmaf(r.rn[2].z, bI, r.rn[1].z * aI));
+                    }
+                    float am = -dla * im, bm = -dlb * im;
+                    V3 ddv = mk(fmaf(r.dir[2].x, bm, r.dir[1].x * am), fmaf(r.dir[2].y, bm, r.dir[1].y * am),
+                                fmaf(r.dir[2].z, bm, r.dir[1].z * am));
+                    obj_add(r.o1, ddw, ddv);
                 }
-                float ra = dla * res_scale(r.dinv[1]), rb = dlb * res_scale(r.dinv[2]);
-                float x = fabsf(ra) > fabsf(rb) ? ra : rb;
-                res = fmaxf(res, x * x);
+                res = fmaxf(res, fmaxf(fabsf(dla * res_scale(r.dinv[1])), fabsf(dlb * res_scale(r.dinv[2]))));
             }
     };
 
@@ -935,7 +1315,17 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
     // then motors 0..8).  The loop is unrolled by two so both orders are
     // straight-line code; each env still stops at its own residual.
     static_assert(PM_SOLVER_ITERATIONS % 2 == 0, "iteration pairs");
+    // the solver stops when max(residual^2) <= 1e-7; tracked as max |residual|
+    // (one v_max with an abs modifier per row) against sqrt(1e-7)
+    constexpr float kResidualAbs = 3.16227766e-4f;
+#ifdef PS_PROFILE_PHASES
+    int prof_it = 0;
+#define PS_COUNT_IT() prof_it++
+#else
+#define PS_COUNT_IT() do {} while (0)
+#endif
     for (int it = 0; it < PM_SOLVER_ITERATIONS; it += 2) {
+        PS_COUNT_IT();
         L = lds.opaque();
         res = 0.0f;
 #pragma unroll
@@ -945,7 +1335,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
             for (int d = 8; d >= 0; d--) limit_row(d);
         }
         contacts();
-        if (res <= (float)PM_SOLVER_RESIDUAL_THRESHOLD) break;
+        if (res <= kResidualAbs) break;
+        PS_COUNT_IT();
         L = lds.opaque();
         res = 0.0f;
         if (__builtin_amdgcn_ballot_w64(lim_on != 0u)) {
@@ -955,10 +1346,24 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
 #pragma unroll
         for (int d = 0; d < 9; d++) motor_row(d);
         contacts();
-        if (res <= (float)PM_SOLVER_RESIDUAL_THRESHOLD) break;
+        if (res <= kResidualAbs) break;
     }
 
     PS_PHASE(4);
+#ifdef PS_PROFILE_PHASES
+    {
+        int wmax = prof_it, wnr = nr;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            wmax = max(wmax, __shfl_xor(wmax, o));
+            wnr = max(wnr, __shfl_xor(wnr, o));
+        }
+        pt.acc[8] += prof_it;
+        pt.acc[9] += wmax;
+        pt.acc[10] += 1;
+        pt.acc[11] += wnr;
+    }
+#endif
     {
         // reload through an opaque address: no store-to-load forwarding, so
         // the registers really were free during the solve
@@ -969,11 +1374,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
             v1[d] = S.stash(9 + d);
             split_dq[d] = S.stash(18 + d);
         }
-        if constexpr (HAS_CUBE) {
-            cw1 = mk(S.stash(27), S.stash(28), S.stash(29));
-            cv1 = mk(S.stash(30), S.stash(31), S.stash(32));
-            cb.pos = mk(S.stash(33), S.stash(34), S.stash(35));
-            cb.quat = Q4{S.stash(36), S.stash(37), S.stash(38), S.stash(39)};
+        if constexpr (NOBJ > 0) {
+            cw1[0] = mk(S.stash(27), S.stash(28), S.stash(29));
+            cv1[0] = mk(S.stash(30), S.stash(31), S.stash(32));
+            bd[0].pos = mk(S.stash(33), S.stash(34), S.stash(35));
+            bd[0].quat = Q4{S.stash(36), S.stash(37), S.stash(38), S.stash(39)};
         }
     }
     // ---- integrate (btMultiBody::stepPositionsMultiDof)
@@ -982,9 +1387,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Cu
         qd[d] = v1[d] + dv[d];
         q[d] += dt * qd[d] + split_dq[d];
     }
-    if constexpr (HAS_CUBE) {
-        cb.omg = cw1 + dw;
-        cb.vel = cv1 + dvl;
+#pragma unroll
+    for (int b = 0; b < NOBJ; b++) {
+        Body &cb = bd[b];
+        cb.omg = cw1[b] + dw[b];
+        cb.vel = cv1[b] + dvl[b];
         cb.pos = cb.pos + cb.vel * dt;
         float ang = norm(cb.omg);
         if (ang * dt > 0.5f * 1.5707963267948966f) ang = 0.5f * 1.5707963267948966f / dt;

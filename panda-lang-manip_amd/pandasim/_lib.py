@@ -19,14 +19,21 @@ ERRORS = {-1: "PS_ERR_ARG", -2: "PS_ERR_HIP", -3: "PS_ERR_UNSUPPORTED"}
 # float row indices of the SoA state (include/pandasim.h)
 F_Q, F_QD, F_MTARGET, F_MKP, F_MKD, F_MVEL, F_MIMP = 0, 9, 18, 27, 36, 45, 54
 F_CPOS, F_CQUAT, F_CVEL, F_COMG = 63, 66, 70, 73
-NUM_FLOAT_ROWS = 76
+F_C2POS, F_C2QUAT, F_C2VEL, F_C2OMG = 76, 79, 83, 86
+OBJECT_ROWS = (F_CPOS, F_C2POS)  # pos, quat (+3), vel (+7), omg (+10) of object 0 / 1
+NUM_FLOAT_ROWS = 89
+NUM_RNG_ROWS = 5
+MAX_GOAL_DIM = 6
+SHAPE_BOX, SHAPE_CYLINDER = 0, 1
 
 
 class Config(C.Structure):
     _fields_ = [
         ("task", C.c_int32), ("control", C.c_int32), ("reward", C.c_int32), ("block_gripper", C.c_int32),
-        ("has_table", C.c_int32), ("has_plane", C.c_int32), ("has_cube", C.c_int32), ("reserved", C.c_int32),
-        ("base", C.c_float * 3), ("cube_half", C.c_float), ("cube_mass", C.c_float),
+        ("has_table", C.c_int32), ("has_plane", C.c_int32), ("n_objects", C.c_int32), ("object_shape", C.c_int32),
+        ("base", C.c_float * 3), ("object_half", C.c_float * 3),
+        ("object_mass", C.c_float), ("object2_mass", C.c_float), ("object_friction", C.c_float),
+        ("table_cx", C.c_float), ("table_hx", C.c_float), ("table_hy", C.c_float),
     ]
 
 
@@ -47,8 +54,9 @@ _lib = None
 def exported_symbols():
     return [
         "ps_abi_version", "ps_default_config", "ps_state_layout", "ps_create", "ps_destroy", "ps_last_error",
-        "ps_obs_dim", "ps_action_dim", "ps_init_state", "ps_reset", "ps_step", "ps_sim_step", "ps_link_state",
-        "ps_inverse_kinematics", "ps_compute_reward", "ps_rng_seed", "ps_rng_uniform", "ps_base_state",
+        "ps_obs_dim", "ps_action_dim", "ps_goal_dim", "ps_max_episode_steps", "ps_init_state", "ps_reset",
+        "ps_step", "ps_sim_step", "ps_link_state", "ps_inverse_kinematics", "ps_compute_reward", "ps_rng_seed",
+        "ps_rng_uniform", "ps_rng_rotation", "ps_base_state",
     ]
 
 
@@ -71,16 +79,19 @@ def lib():
     L.ps_last_error.restype = C.c_char_p
     L.ps_obs_dim.argtypes = [V]
     L.ps_action_dim.argtypes = [V]
+    L.ps_goal_dim.argtypes = [V]
+    L.ps_max_episode_steps.argtypes = [V]
     L.ps_init_state.argtypes = [V, V, V]
     L.ps_reset.argtypes = [V, V, V, V, V, V, V, V]
     L.ps_step.argtypes = [V, V, V, V, V, V, V, V, V, I, V, V, V]
     L.ps_sim_step.argtypes = [V, V, I, V]
     L.ps_link_state.argtypes = [V, V, I, V, V, V, V, V]
     L.ps_inverse_kinematics.argtypes = [V, V, I, V, V, V, V]
-    L.ps_compute_reward.argtypes = [I, V, I, V, I, V, V, I64, V]
+    L.ps_compute_reward.argtypes = [I, I, V, I, V, I, V, V, I64, V]
     L.ps_rng_seed.argtypes = [V, V, V, V, V]
     L.ps_rng_uniform.argtypes = [V, V, V, I, P(C.c_double), P(C.c_double), V, V]
-    L.ps_base_state.argtypes = [V, V, V, V, V, V, V, V]
+    L.ps_rng_rotation.argtypes = [V, V, V, V, V]
+    L.ps_base_state.argtypes = [V, V, I, V, V, V, V, V, V]
     for name in exported_symbols():
         getattr(L, name).restype = getattr(L, name).restype if name in ("ps_destroy", "ps_last_error") else I
     _lib = L

@@ -10,7 +10,7 @@
   continues each env's generator (the reference would draw OS entropy).
 * ``step`` returns ``(obs, reward, terminated, truncated, info)`` with
   terminated = is_success, reward from compute_reward, truncated from the
-  TimeLimit(50) of the registration (__init__.py:18-40).  With ``autoreset``
+  TimeLimit of the registration (50 steps, Stack 100; __init__.py:18-46).  With ``autoreset``
   (default) finished envs are reset inside the kernel; ``info`` then carries
   ``final_observation``/``final_achieved_goal`` for them.
 * ``compute_reward(ag, dg, info)`` is vectorised over leading dims (HER).
@@ -26,18 +26,15 @@ import torch
 from . import _lib as L
 from .sim import PandaSim, _ptr
 
-MAX_EPISODE_STEPS = 50
-
-
-def _spaces(obs_dim: int, action_dim: int):
+def _spaces(obs_dim: int, action_dim: int, goal_dim: int = 3):
     try:
         from gymnasium import spaces  # optional: not installed in the build image
     except Exception:  # pragma: no cover - depends on the environment
         return None, None
     obs = spaces.Dict(dict(
         observation=spaces.Box(-10.0, 10.0, shape=(obs_dim,), dtype=np.float32),
-        desired_goal=spaces.Box(-10.0, 10.0, shape=(3,), dtype=np.float32),
-        achieved_goal=spaces.Box(-10.0, 10.0, shape=(3,), dtype=np.float32),
+        desired_goal=spaces.Box(-10.0, 10.0, shape=(goal_dim,), dtype=np.float32),
+        achieved_goal=spaces.Box(-10.0, 10.0, shape=(goal_dim,), dtype=np.float32),
     ))
     return obs, spaces.Box(-1.0, 1.0, shape=(action_dim,), dtype=np.float32)
 
@@ -53,14 +50,15 @@ class PandaVecEnv:
         self.device = self.sim.device
         self.autoreset = autoreset
         self.obs_dim, self.action_dim = self.sim.obs_dim, self.sim.action_dim
-        self.observation_space, self.action_space = _spaces(self.obs_dim, self.action_dim)
-        self.max_episode_steps = MAX_EPISODE_STEPS
-        B, dev = self.num_envs, self.device
+        self.goal_dim = self.sim.goal_dim
+        self.observation_space, self.action_space = _spaces(self.obs_dim, self.action_dim, self.goal_dim)
+        self.max_episode_steps = self.sim.max_episode_steps
+        B, dev, G = self.num_envs, self.device, self.goal_dim
         self._obs = torch.zeros(B, self.obs_dim, device=dev)
-        self._ag = torch.zeros(B, 3, device=dev)
-        self._dg = torch.zeros(B, 3, device=dev)
+        self._ag = torch.zeros(B, G, device=dev)
+        self._dg = torch.zeros(B, G, device=dev)
         self._final_obs = torch.zeros(B, self.obs_dim, device=dev)
-        self._final_ag = torch.zeros(B, 3, device=dev)
+        self._final_ag = torch.zeros(B, G, device=dev)
         self._reward = torch.zeros(B, device=dev)
         self._term = torch.zeros(B, dtype=torch.uint8, device=dev)
         self._trunc = torch.zeros(B, dtype=torch.uint8, device=dev)
@@ -89,7 +87,7 @@ class PandaVecEnv:
         self.sim._call("ps_reset", self.sim._ctx, _ptr(self.sim.state), _ptr(m), _ptr(seeds), _ptr(self._obs),
                        _ptr(self._ag), _ptr(self._dg), self.sim._stream())
         self._has_reset = True
-        info = {"is_success": self.compute_success(self._ag, self.sim.goal[:, :self.num_envs].t())}
+        info = {"is_success": self.compute_success(self._ag, self.sim.goals())}
         return self._obs_dict(), info
 
     def step(self, actions, copy: bool = True) -> Tuple[Dict[str, torch.Tensor], torch.Tensor, torch.Tensor,
@@ -126,20 +124,9 @@ class PandaVecEnv:
         return self._reward_and_success(achieved_goal, desired_goal)[1]
 
     def _reward_and_success(self, achieved_goal, desired_goal):
-        ag = torch.as_tensor(achieved_goal, device=self.device)
-        dg = torch.as_tensor(desired_goal, device=self.device)
-        lead = ag.shape[:-1]
-        adbl, ddbl = ag.dtype == torch.float64, dg.dtype == torch.float64
-        ag = (ag if adbl else ag.to(torch.float32)).reshape(-1, 3).contiguous()
-        dg = (dg if ddbl else dg.to(torch.float32)).reshape(-1, 3).contiguous()
-        n = ag.shape[0]
-        r = torch.empty(n, device=self.device)
-        s = torch.empty(n, dtype=torch.uint8, device=self.device)
-        with torch.cuda.device(self.device):
-            rc = self.sim._lib.ps_compute_reward(0 if self.reward_type == "sparse" else 1, _ptr(ag), int(adbl),
-                                                 _ptr(dg), int(ddbl), _ptr(r), _ptr(s), n, self.sim._stream())
-        L.check(rc, what="ps_compute_reward")
-        return r.reshape(lead), s.bool().reshape(lead)
+        from .utils import goal_reward_and_success
+
+        return goal_reward_and_success(achieved_goal, desired_goal, self.reward_type, task=self.task_name)
 
     # ------------------------------------------------------- state snapshots
     def save_state(self) -> int:
@@ -161,8 +148,8 @@ class PandaVecEnv:
 
 # ------------------------------------------------------------- registration
 # panda_gym/__init__.py:8-54: 6 tasks x {sparse, dense} x {ee, joints}
-_TASK_IDS = {"Reach": "reach", "Push": "push", "PickAndPlace": "pick_and_place",
-             "Slide": None, "Stack": None, "Flip": None}
+_TASK_IDS = {"Reach": "reach", "Push": "push", "Slide": "slide", "PickAndPlace": "pick_and_place",
+             "Stack": "stack", "Flip": "flip"}
 REGISTRY: Dict[str, Dict[str, Any]] = {}
 for _reward in ("sparse", "dense"):
     for _control in ("ee", "joints"):
@@ -183,8 +170,6 @@ def make(env_id: str, num_envs: int = 1, device="cuda", fused: bool = True, **kw
     if env_id not in REGISTRY:
         raise KeyError(f"unknown env id {env_id}")
     spec = REGISTRY[env_id]
-    if spec["task"] is None:
-        raise NotImplementedError(f"{env_id}: Slide/Stack/Flip are the next rows of SURVEY.md §8(f)")
     if not fused:
         from .core import TimeLimit
         from .panda_tasks import ENV_CLASSES

@@ -18,7 +18,7 @@ import torch
 
 from . import _lib as L
 
-TASKS = {"reach": 0, "push": 1, "pick_and_place": 2}
+TASKS = {"reach": 0, "push": 1, "pick_and_place": 2, "slide": 3, "stack": 4, "flip": 5}
 CONTROLS = {"ee": 0, "joints": 1}
 REWARDS = {"sparse": 0, "dense": 1}
 JOINT_TO_DOF = {0: 0, 1: 1, 2: 2, 3: 3, 4: 4, 5: 5, 6: 6, 9: 7, 10: 8}
@@ -46,17 +46,20 @@ class PandaSim:
         elif task is None:
             # empty world, built up by loadURDF/create_* as PyBullet() + Robot/Task constructors do
             self.cfg = L.default_config(0, 0, 0)
-            self.cfg.has_table = self.cfg.has_plane = self.cfg.has_cube = 0
+            self.cfg.has_table = self.cfg.has_plane = self.cfg.n_objects = 0
             self.cfg.base[0] = 0.0
         else:
             self.cfg = L.default_config(TASKS[task], CONTROLS[control_type], REWARDS[reward_type])
         self._lib = L.lib()
         self._ctx = None
         self._create_ctx()
-        # body name -> kind ("robot", "object", "ghost"); the registered tasks' names
+        # body name -> kind ("robot", "object", "ghost"); objects -> their index
         self._bodies: Dict[str, str] = {"panda": "robot"}
-        if self.cfg.has_cube:
-            self._bodies["object"] = "object"
+        self._objects: Dict[str, int] = {}
+        names = {0: [], 1: ["object"], 2: ["object1", "object2"]}[self.cfg.n_objects]
+        for k, name in enumerate(names):
+            self._bodies[name] = "object"
+            self._objects[name] = k
         self._ghost_pos: Dict[str, torch.Tensor] = {}
         self._ghost_orn: Dict[str, torch.Tensor] = {}
         self.layout = L.layout(self.num_envs)
@@ -83,8 +86,9 @@ class PandaSim:
         n = lay.stride
         self.f = s[lay.float_offset:lay.float_offset + L.NUM_FLOAT_ROWS * n * 4].view(torch.float32).view(
             L.NUM_FLOAT_ROWS, n)
-        self.goal = s[lay.goal_offset:lay.goal_offset + 3 * n * 8].view(torch.float64).view(3, n)
-        self.rng = s[lay.rng_offset:lay.rng_offset + 4 * n * 8].view(torch.int64).view(4, n)
+        self.goal = s[lay.goal_offset:lay.goal_offset + L.MAX_GOAL_DIM * n * 8].view(torch.float64).view(
+            L.MAX_GOAL_DIM, n)
+        self.rng = s[lay.rng_offset:lay.rng_offset + L.NUM_RNG_ROWS * n * 8].view(torch.int64).view(L.NUM_RNG_ROWS, n)
         self.elapsed = s[lay.elapsed_offset:lay.elapsed_offset + n * 4].view(torch.int32)
 
     def _stream(self):
@@ -112,6 +116,18 @@ class PandaSim:
     @property
     def action_dim(self) -> int:
         return self._lib.ps_action_dim(self._ctx)
+
+    @property
+    def goal_dim(self) -> int:
+        return self._lib.ps_goal_dim(self._ctx)
+
+    @property
+    def max_episode_steps(self) -> int:
+        return self._lib.ps_max_episode_steps(self._ctx)
+
+    def goals(self) -> torch.Tensor:
+        """[B, goal_dim] float64 view-copy of the fused path's goals."""
+        return self.goal[:self.goal_dim, :self.num_envs].t()
 
     @property
     def dt(self) -> float:
@@ -163,31 +179,59 @@ class PandaSim:
 
     def create_table(self, length: float, width: float, height: float, x_offset: float = 0.0,
                      lateral_friction=None, spinning_friction=None) -> None:
-        """pybullet.py:741-771."""
-        if (length, width, height, x_offset) != TABLE or lateral_friction is not None or spinning_friction is not None:
-            raise NotImplementedError(f"create_table{(length, width, height, x_offset)}: only {TABLE} is compiled in")
+        """pybullet.py:741-771: a static box with its top at z = 0 (default friction)."""
+        if lateral_friction is not None or spinning_friction is not None:
+            raise NotImplementedError("create_table: only the default table friction is compiled in")
         self.cfg.has_table = 1
+        self.cfg.table_cx, self.cfg.table_hx, self.cfg.table_hy = float(x_offset), length / 2, width / 2
         self._create_ctx()
+
+    def _add_object(self, body_name: str, shape: int, half, mass: float, lateral_friction, position) -> None:
+        n = self.cfg.n_objects
+        fric = 0.5 if lateral_friction is None else float(lateral_friction)
+        if n >= 2 or mass <= 0:
+            raise NotImplementedError("at most two dynamic objects (Stack) are compiled in")
+        if n == 1 and (shape != self.cfg.object_shape or [float(h) for h in half] != list(self.cfg.object_half)
+                       or fric != self.cfg.object_friction or shape != L.SHAPE_BOX):
+            raise NotImplementedError("a second object must be a cube like the first (Stack)")
+        if shape == L.SHAPE_BOX and max(half) != min(half):
+            raise NotImplementedError("boxes must be cubes (isotropic inertia)")
+        self.cfg.object_shape = shape
+        for k in range(3):
+            self.cfg.object_half[k] = float(half[k])
+        self.cfg.object_friction = fric
+        if n == 0:
+            self.cfg.object_mass = float(mass)
+        else:
+            self.cfg.object2_mass = float(mass)
+        self.cfg.n_objects = n + 1
+        # the fused-kernel task matching the scene (the plugin path ignores it)
+        self.cfg.task = {1: TASKS["slide"] if shape == L.SHAPE_CYLINDER else TASKS["push"], 2: TASKS["stack"]}[n + 1]
+        self._bodies[body_name] = "object"
+        self._objects[body_name] = n
+        self._create_ctx()
+        self.set_base_pose(body_name, position, [0.0, 0.0, 0.0, 1.0])
 
     def create_box(self, body_name: str, half_extents, mass: float, position, rgba_color=None, specular_color=None,
                    ghost: bool = False, lateral_friction=None, spinning_friction=None, texture=None) -> None:
-        """pybullet.py:584-626: the one dynamic cube of Push/PickAndPlace, or a ghost marker."""
+        """pybullet.py:516-582: a dynamic cube (Push/PickAndPlace/Flip; two for Stack) or a ghost marker."""
         if ghost:
             self._add_ghost(body_name, position)
             return
-        he = [float(x) for x in half_extents]
-        if self.cfg.has_cube or max(he) != min(he) or mass <= 0 or lateral_friction is not None \
-                or spinning_friction is not None:
-            raise NotImplementedError("create_box: one dynamic cube (equal half extents, default friction) is "
-                                      "compiled in")
-        self.cfg.has_cube = 1
-        self.cfg.cube_half = he[0]
-        self.cfg.cube_mass = float(mass)
-        if self.cfg.task == 0:
-            self.cfg.task = 1
-        self._bodies[body_name] = "object"
-        self._create_ctx()
-        self.set_base_pose(body_name, position, [0.0, 0.0, 0.0, 1.0])
+        if spinning_friction is not None:
+            raise NotImplementedError("create_box: spinning friction of objects is not modelled")
+        self._add_object(body_name, L.SHAPE_BOX, [float(x) for x in half_extents], mass, lateral_friction, position)
+
+    def create_cylinder(self, body_name: str, radius: float, height: float, mass: float, position, rgba_color=None,
+                        specular_color=None, ghost: bool = False, lateral_friction=None,
+                        spinning_friction=None) -> None:
+        """pybullet.py:584-623: the upright cylinder of Slide (axis z), or a ghost marker."""
+        if ghost:
+            self._add_ghost(body_name, position)
+            return
+        if spinning_friction is not None:
+            raise NotImplementedError("create_cylinder: spinning friction of objects is not modelled")
+        self._add_object(body_name, L.SHAPE_CYLINDER, [radius, radius, height / 2], mass, lateral_friction, position)
 
     def create_sphere(self, body_name: str, radius: float, mass: float, position, rgba_color=None,
                       specular_color=None, ghost: bool = False) -> None:
@@ -195,10 +239,6 @@ class PandaSim:
         if not ghost:
             raise NotImplementedError("create_sphere: only ghost spheres (targets) are supported")
         self._add_ghost(body_name, position)
-
-    def create_cylinder(self, *args, **kwargs) -> None:
-        """pybullet.py:628-663 (Slide): SURVEY.md §8(f), not built yet."""
-        raise NotImplementedError("create_cylinder: PandaSlide is a next row of SURVEY.md §8(f)")
 
     def set_lateral_friction(self, body: str, link: int, lateral_friction: float) -> None:
         """pybullet.py:773-785: the compiled-in gripper proxies carry panda.py:47-48's values."""
@@ -228,6 +268,13 @@ class PandaSim:
         seeds = torch.as_tensor(seeds, device=self.device).to(torch.int64).reshape(self.num_envs).contiguous()
         m = None if mask is None else torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
         self._call("ps_rng_seed", self._ctx, _ptr(self.state), _ptr(m), _ptr(seeds), self._stream())
+
+    def random_rotation(self, mask=None) -> torch.Tensor:
+        """Rotation.random().as_quat() of every env's Flip goal stream -> [B, 4] float64."""
+        out = torch.empty(self.num_envs, 4, dtype=torch.float64, device=self.device)
+        m = None if mask is None else torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        self._call("ps_rng_rotation", self._ctx, _ptr(self.state), _ptr(m), _ptr(out), self._stream())
+        return out
 
     def uniform(self, low, high, mask=None) -> torch.Tensor:
         """Generator.uniform(low, high) of every env's own PCG64 stream -> [B, n] float64."""
@@ -293,12 +340,15 @@ class PandaSim:
     def get_joint_velocity(self, body: str, joint: int) -> torch.Tensor:
         return self.f[L.F_QD + JOINT_TO_DOF[joint], :self.num_envs].clone()
 
-    def _base_state(self):
+    def _object_rows(self, body: str) -> int:
+        return L.OBJECT_ROWS[self._objects[body]]
+
+    def _base_state(self, body: str):
         B = self.num_envs
         pos, euler, vel, avel = (torch.empty(B, 3, device=self.device) for _ in range(4))
         quat = torch.empty(B, 4, device=self.device)
-        self._call("ps_base_state", self._ctx, _ptr(self.state), _ptr(pos), _ptr(quat), _ptr(euler), _ptr(vel),
-                   _ptr(avel), self._stream())
+        self._call("ps_base_state", self._ctx, _ptr(self.state), self._objects[body], _ptr(pos), _ptr(quat),
+                   _ptr(euler), _ptr(vel), _ptr(avel), self._stream())
         return pos, quat, euler, vel, avel
 
     def get_base_position(self, body: str) -> torch.Tensor:
@@ -308,7 +358,7 @@ class PandaSim:
             return self._ghost_pos[body].clone()
         if kind == "robot":
             return torch.tensor([float(x) for x in self.cfg.base], device=self.device).expand(self.num_envs, 3)
-        return self.rows(L.F_CPOS, 3).clone()
+        return self.rows(self._object_rows(body), 3).clone()
 
     def get_base_orientation(self, body: str) -> torch.Tensor:
         """getBasePositionAndOrientation[1] (pybullet.py:296-306), (x, y, z, w)."""
@@ -317,7 +367,7 @@ class PandaSim:
             return self._ghost_orn[body].clone()
         if kind == "robot":
             return torch.tensor([0.0, 0.0, 0.0, 1.0], device=self.device).expand(self.num_envs, 4)
-        return self.rows(L.F_CQUAT, 4).clone()
+        return self.rows(self._object_rows(body) + 3, 4).clone()
 
     def get_base_rotation(self, body: str, type: str = "euler") -> torch.Tensor:
         """pybullet.py:308-325: getEulerFromQuaternion of the base orientation."""
@@ -326,20 +376,20 @@ class PandaSim:
         if type != "euler":
             raise ValueError("""type must be "euler" or "quaternion".""")
         if self._kind(body) == "object":
-            return self._base_state()[2]
+            return self._base_state(body)[2]
         return euler_from_quaternion(self.get_base_orientation(body))
 
     def get_base_velocity(self, body: str) -> torch.Tensor:
         """getBaseVelocity[0] (pybullet.py:327-337)."""
         if self._kind(body) != "object":
             return torch.zeros(self.num_envs, 3, device=self.device)
-        return self.rows(L.F_CVEL, 3).clone()
+        return self.rows(self._object_rows(body) + 7, 3).clone()
 
     def get_base_angular_velocity(self, body: str) -> torch.Tensor:
         """getBaseVelocity[1] (pybullet.py:339-349)."""
         if self._kind(body) != "object":
             return torch.zeros(self.num_envs, 3, device=self.device)
-        return self.rows(L.F_COMG, 3).clone()
+        return self.rows(self._object_rows(body) + 10, 3).clone()
 
     # -------------------------------------------------------------- setters
     def set_joint_angles(self, body: str, joints: Sequence[int], angles) -> None:
@@ -368,8 +418,9 @@ class PandaSim:
             self._ghost_pos[body][:] = pos.expand(self.num_envs, 3)
             self._ghost_orn[body][:] = orientation.expand(self.num_envs, 4)
             return
-        self.set_rows(L.F_CPOS, torch.as_tensor(position, device=self.device).to(torch.float32))
-        self.set_rows(L.F_CQUAT, orientation.to(torch.float32))
+        row = self._object_rows(body)
+        self.set_rows(row, torch.as_tensor(position, device=self.device).to(torch.float32))
+        self.set_rows(row + 3, orientation.to(torch.float32))
 
     def control_joints(self, body: str, joints: Sequence[int], target_angles, forces) -> None:
         """setJointMotorControlArray(POSITION_CONTROL) (pybullet.py:462-477)."""
@@ -395,7 +446,6 @@ class PandaSim:
 
 # ---------------------------------------------------------------- helpers
 PLANE_Z = -0.4                      # tasks/*.py: create_plane(z_offset=-0.4)
-TABLE = (1.1, 0.7, 0.4, -0.3)       # tasks/*.py: create_table(length, width, height, x_offset)
 
 
 def euler_from_quaternion(q: torch.Tensor) -> torch.Tensor:

@@ -1,9 +1,8 @@
-# GPU pass: phase split of the fused step kernel (diagnostic build) + bench line
+# GPU pass: phase split of the fused step kernel (diagnostic build)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 300 python scripts/phase_profile.py PandaPush-v3 65536 20 > gpurun_out/phase.log 2>&1 && \
 timeout -k 10 300 python scripts/phase_profile.py PandaReach-v3 65536 20 >> gpurun_out/phase.log 2>&1 && \
-timeout -k 10 300 python scripts/phase_profile.py PandaPickAndPlace-v3 65536 20 >> gpurun_out/phase.log 2>&1 && \
-timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench.log 2>&1
+timeout -k 10 300 python scripts/phase_profile.py PandaPickAndPlace-v3 65536 20 >> gpurun_out/phase.log 2>&1
 echo "done rc=$?"

@@ -27,7 +27,7 @@ def main():
     env.reset(seed=12345)
     lib = L.lib()
     lib.ps_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int]
-    buf = (C.c_ulonglong * 8)()
+    buf = (C.c_ulonglong * 12)()
     g = torch.Generator(device="cuda")
     g.manual_seed(0xC0FFEE)
     for k in range(5):
@@ -38,11 +38,14 @@ def main():
         env.step(torch.rand(B, env.action_dim, device="cuda", generator=g) * 2 - 1, copy=False)
     torch.cuda.synchronize()
     assert lib.ps_debug_phase_cycles(buf, 0) == 0
-    tot = sum(buf)
+    tot = sum(buf[:8])
     waves = (B + 63) // 64
     print(f"{env_id} B={B}: {tot / waves / steps:.0f} wave-cycles per env-step")
-    for n, v in zip(NAMES, buf):
+    for n, v in zip(NAMES, buf[:8]):
         print(f"  {n:24s} {v / tot * 100:6.2f} %   {v / waves / steps / 20:10.0f} cyc/substep-equiv")
+    subs = buf[10]  # wave-substeps counted by lane 0 of each wave
+    print(f"  PGS iterations per substep: lane-0 mean {buf[8] / subs:.2f}, wave max {buf[9] / subs:.2f}; "
+          f"max robot contacts per wave {buf[11] / subs:.2f}")
 
 
 if __name__ == "__main__":

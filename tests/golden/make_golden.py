@@ -84,9 +84,12 @@ def main():
     sys.dont_write_bytecode = True
     _placeholder_modules()
     sys.path.insert(0, REF)
+    from panda_gym.envs.tasks.flip import Flip
     from panda_gym.envs.tasks.pick_and_place import PickAndPlace
     from panda_gym.envs.tasks.push import Push
     from panda_gym.envs.tasks.reach import Reach
+    from panda_gym.envs.tasks.slide import Slide
+    from panda_gym.envs.tasks.stack import Stack
 
     seeds = [0, 1, 2, 7, 42, 6789, 12345, 13795, 657894, 794512, 2**31 - 1, 2**32 - 1, 2**32, 2**40 + 3,
              2**63 + 11, 2**64 - 1] + list(range(100, 300))
@@ -135,6 +138,58 @@ def main():
     out["her_dg"] = dg3
     out["her_reward_sparse"] = np.asarray(Push(sim, reward_type="sparse").compute_reward(ag3, dg3, {}), np.float32)
     out["her_reward_dense"] = np.asarray(Push(sim, reward_type="dense").compute_reward(ag3, dg3, {}), np.float32)
+
+    # --- Slide, Stack, Flip (draws from task.np_random).
+    # Flip's goal comes from scipy's Rotation.random() on numpy's unseeded
+    # global RandomState (flip.py:70-72): only its object draws are seeded.
+    for name, cls in [("slide", Slide), ("stack", Stack), ("flip", Flip)]:
+        goals = np.zeros((len(seeds), n_resets, 6 if cls is Stack else 3))
+        objs = np.zeros((len(seeds), n_resets, 6 if cls is Stack else 3))
+        for i, s in enumerate(seeds):
+            sim = RecorderSim()
+            task = cls(sim)
+            task.np_random = seeded_rng(int(s))
+            for r in range(n_resets):
+                task.reset()
+                if cls is Stack:
+                    goals[i, r] = task.goal
+                    objs[i, r, :3] = sim.poses["object1"][0]
+                    objs[i, r, 3:] = sim.poses["object2"][0]
+                elif cls is Slide:
+                    goals[i, r] = task.goal
+                    objs[i, r] = sim.poses["object"][0]
+                else:
+                    objs[i, r] = sim.poses["object"][0]
+                    assert np.array_equal(sim.poses["object"][1], np.zeros(3))  # Euler zeros
+        if cls is not Flip:
+            out[f"{name}_goal"] = goals
+        out[f"{name}_object"] = objs
+
+    rng = np.random.default_rng(2025)
+    # Stack: 6-D goals, threshold 0.1 (stack.py:118-131)
+    dg6 = rng.uniform(-0.2, 0.2, size=(n, 6))
+    ag6 = (dg6 + rng.normal(scale=0.04, size=(n, 6))).astype(np.float32)
+    dir6 = rng.normal(size=(512, 6))
+    dir6 /= np.linalg.norm(dir6, axis=1, keepdims=True)
+    ag6[:512] = (dg6[:512] + dir6 * (0.1 + rng.uniform(-1e-6, 1e-6, size=(512, 1)))).astype(np.float32)
+    out["stack_ag"], out["stack_dg"] = ag6, dg6
+    for reward_type in ["sparse", "dense"]:
+        task = Stack(RecorderSim(), reward_type=reward_type)
+        out[f"stack_reward_{reward_type}"] = np.asarray(task.compute_reward(ag6, dg6, {}), dtype=np.float32)
+        out["stack_success"] = np.asarray(task.is_success(ag6, dg6), dtype=np.bool_)
+    # Flip: angle_distance on single (float32 achieved, float64 desired)
+    # quaternion pairs, as RobotTaskEnv.step calls it (core.py:285-288);
+    # batched inputs would hit np.inner's outer-product semantics (utils.py:29)
+    qd = rng.normal(size=(n, 4))
+    qd /= np.linalg.norm(qd, axis=1, keepdims=True)
+    qa = qd + rng.normal(scale=0.3, size=(n, 4))
+    qa = (qa / np.linalg.norm(qa, axis=1, keepdims=True)).astype(np.float32)
+    out["flip_ag"], out["flip_dg"] = qa, qd
+    for reward_type in ["sparse", "dense"]:
+        task = Flip(RecorderSim(), reward_type=reward_type)
+        out[f"flip_reward_{reward_type}"] = np.array([task.compute_reward(a, d, {}) for a, d in zip(qa, qd)],
+                                                     dtype=np.float32)
+        out["flip_success"] = np.array([task.is_success(a, d) for a, d in zip(qa, qd)], dtype=np.bool_)
     np.savez_compressed(OUT, **out)
     print("wrote", OUT, {k: v.shape for k, v in out.items()})
 

@@ -3,7 +3,8 @@ state buffer and the oracle's per-env structs."""
 import numpy as np
 import oracle as O
 
-TASK_NAMES = ["reach", "push", "pick_and_place"]
+TASK_NAMES = ["reach", "push", "pick_and_place", "slide", "stack", "flip"]
+OBJECT_ROWS = (63, 76)
 
 
 def oracle_config_for(sim_cfg):
@@ -11,11 +12,13 @@ def oracle_config_for(sim_cfg):
     cfg = O.config(TASK_NAMES[sim_cfg.task], control="ee" if sim_cfg.control == 0 else "joints",
                    reward="sparse" if sim_cfg.reward == 0 else "dense")
     cfg.block_gripper = sim_cfg.block_gripper
-    cfg.has_table, cfg.has_plane, cfg.has_cube = sim_cfg.has_table, sim_cfg.has_plane, sim_cfg.has_cube
+    cfg.has_table, cfg.has_plane = sim_cfg.has_table, sim_cfg.has_plane
+    cfg.n_objects, cfg.object_shape = sim_cfg.n_objects, sim_cfg.object_shape
     for k in range(3):
         cfg.base[k] = float(np.float32(sim_cfg.base[k]))
-    cfg.cube_half = float(np.float32(sim_cfg.cube_half))
-    cfg.cube_mass = float(np.float32(sim_cfg.cube_mass))
+        cfg.object_half[k] = float(np.float32(sim_cfg.object_half[k]))
+    for name in ("object_mass", "object2_mass", "object_friction", "table_cx", "table_hx", "table_hy"):
+        setattr(cfg, name, float(np.float32(getattr(sim_cfg, name))))
     return cfg
 
 
@@ -37,11 +40,15 @@ def oracle_env_from(cfg, snap, i):
         env.q[d], env.qd[d] = f[d], f[9 + d]
         env.m_target[d], env.m_kp[d], env.m_kd[d] = f[18 + d], f[27 + d], f[36 + d]
         env.m_vel[d], env.m_maximp[d] = f[45 + d], f[54 + d]
-    for k in range(3):
-        env.cpos[k], env.cvel[k], env.comg[k] = f[63 + k], f[70 + k], f[73 + k]
+    for b, r in enumerate(OBJECT_ROWS):
+        o = env.obj[b]
+        for k in range(3):
+            o.pos[k], o.vel[k], o.omg[k] = f[r + k], f[r + 7 + k], f[r + 10 + k]
+        for k in range(4):
+            o.quat[k] = f[r + 3 + k]
+    for k in range(snap["goal"].shape[0]):
         env.goal[k] = snap["goal"][k, i]
-    for k in range(4):
-        env.cquat[k] = f[66 + k]
+    for k in range(snap["rng"].shape[0]):
         env.rng[k] = int(snap["rng"][k, i])
     env.elapsed = int(snap["elapsed"][i])
     return env

@@ -33,26 +33,32 @@ def test_library_exports_every_header_symbol(L):
 
 
 def test_abi_version(L):
-    assert L.lib().ps_abi_version() == 1
+    assert L.lib().ps_abi_version() == 2
 
 
 def test_state_layout(L):
     lay = L.layout(1000)
     assert lay.stride == 1024
-    assert lay.goal_offset == 76 * 1024 * 4
-    assert lay.rng_offset == lay.goal_offset + 3 * 1024 * 8
-    assert lay.total_bytes == lay.rng_offset + 4 * 1024 * 8 + 1024 * 4
+    assert lay.goal_offset == 89 * 1024 * 4
+    assert lay.rng_offset == lay.goal_offset + 6 * 1024 * 8
+    assert lay.total_bytes == lay.rng_offset + 5 * 1024 * 8 + 1024 * 4
     assert lay.goal_offset % 8 == 0 and lay.rng_offset % 8 == 0
 
 
 def test_default_configs(L):
-    for task in range(3):
+    for task in range(6):
         cfg = L.default_config(task, 0, 1)
-        assert cfg.block_gripper == (task != 2)  # panda_tasks.py:46,62,78
-        assert cfg.has_cube == (task != 0)
+        # panda_tasks.py:26,43,60,77,94,111: the gripper is free for PickAndPlace, Stack, Flip
+        assert cfg.block_gripper == (task in (0, 1, 3))
+        assert cfg.n_objects == {0: 0, 4: 2}.get(task, 1)
+        assert cfg.object_shape == (L.SHAPE_CYLINDER if task == 3 else L.SHAPE_BOX)
         assert abs(cfg.base[0] + 0.6) < 1e-7
+    slide = L.default_config(3, 0, 0)
+    assert abs(slide.object_friction - 0.04) < 1e-7 and abs(slide.table_hx - 0.7) < 1e-7  # slide.py:33-42
+    stack = L.default_config(4, 0, 0)
+    assert (stack.object_mass, stack.object2_mass) == (2.0, 1.0)  # stack.py:33-52
     bad = L.Config()
-    assert L.lib().ps_default_config(5, 0, 0, C.byref(bad)) < 0
+    assert L.lib().ps_default_config(6, 0, 0, C.byref(bad)) < 0
 
 
 def test_create_and_dims_without_gpu(L):
@@ -67,6 +73,24 @@ def test_create_and_dims_without_gpu(L):
     assert lib.ps_obs_dim(ctx) == 6 and lib.ps_action_dim(ctx) == 7
     lib.ps_destroy(ctx)
     assert lib.ps_create(C.byref(cfg), 0, 0, C.byref(ctx)) < 0
+    # goal sizes and TimeLimits of every task (__init__.py:18-46)
+    dims = {0: (6, 3, 50), 1: (18, 3, 50), 2: (19, 3, 50), 3: (18, 3, 50), 4: (31, 6, 100), 5: (20, 4, 50)}
+    for task, (obs, goal, steps) in dims.items():
+        cfg = L.default_config(task, 0, 0)
+        assert lib.ps_create(C.byref(cfg), 8, 0, C.byref(ctx)) == 0
+        assert (lib.ps_obs_dim(ctx), lib.ps_goal_dim(ctx), lib.ps_max_episode_steps(ctx)) == (obs, goal, steps)
+        lib.ps_destroy(ctx)
+
+
+def test_create_rejects_uncompiled_scenes(L):
+    lib = L.lib()
+    ctx = C.c_void_p()
+    cfg = L.default_config(1, 0, 0)
+    cfg.object_half[2] = 0.05                      # a non-cube box
+    assert lib.ps_create(C.byref(cfg), 8, 0, C.byref(ctx)) < 0
+    cfg = L.default_config(4, 0, 0)
+    cfg.object_shape = L.SHAPE_CYLINDER            # two cylinders
+    assert lib.ps_create(C.byref(cfg), 8, 0, C.byref(ctx)) < 0
 
 
 def test_registry_has_all_24_ids():
@@ -76,8 +100,8 @@ def test_registry_has_all_24_ids():
     assert REGISTRY["PandaPushJointsDense-v3"] == dict(task="push", reward_type="dense", control_type="joints",
                                                        max_episode_steps=50)
     assert REGISTRY["PandaStack-v3"]["max_episode_steps"] == 100
-    with pytest.raises(NotImplementedError):
-        make("PandaSlide-v3")
+    with pytest.raises(KeyError):
+        make("PandaSlide-v2")
 
 
 def test_no_silent_cpu_fallback():

@@ -20,8 +20,10 @@ import oracle as O
 
 pytestmark = pytest.mark.gpu
 
-TASKS = [("reach", "ee"), ("reach", "joints"), ("push", "ee"), ("push", "joints"), ("pick_and_place", "ee"),
-         ("pick_and_place", "joints")]
+ALL_TASKS = ["reach", "push", "pick_and_place", "slide", "stack", "flip"]
+OBJECT_TASKS = ALL_TASKS[1:]
+TASKS = [(t, c) for t in ALL_TASKS for c in ("ee", "joints")]
+FREE_GRIPPER = ("pick_and_place", "stack", "flip")  # panda_tasks.py:26,43,111
 
 
 @pytest.fixture(scope="module")
@@ -87,18 +89,35 @@ def test_kat_box_free_fall(ps):  # pybullet_test.py:56-64 (robot parked far away
 
 
 # ------------------------------------------------------------ task layer
-@pytest.mark.parametrize("task", ["reach", "push", "pick_and_place"])
+@pytest.mark.parametrize("task", ALL_TASKS)
 def test_reset_goldens_bit_exact(ps, golden, task):
+    """Goal and object draws of 216 seeds x 4 successive resets against the
+    reference's own numpy draws (tests/golden/make_golden.py).  Flip's goal is
+    the reference's unseeded Rotation.random(); it is checked against the
+    oracle's auxiliary stream instead (parity of the restatement)."""
     seeds = golden["seeds"]
-    env = make_env(ps, task, "ee", len(seeds))
-    for r in range(golden[f"{task}_goal"].shape[1]):
+    B = len(seeds)
+    env = make_env(ps, task, "ee", B)
+    G = env.goal_dim
+    cfg = oracle_config_for(env.sim.cfg)
+    oenvs = [O.new_env(cfg) for _ in range(B)]
+    for r in range(golden[f"{task}_object"].shape[1]):
         obs, _ = env.reset(seed=seeds if r == 0 else None)
-        goal = env.sim.goal[:, :len(seeds)].t().cpu().numpy()
-        assert np.array_equal(goal, golden[f"{task}_goal"][:, r])
-        assert np.array_equal(obs["desired_goal"].cpu().numpy(), golden[f"{task}_goal"][:, r].astype(np.float32))
+        goal = env.sim.goal[:G, :B].t().cpu().numpy()
+        if task == "flip":
+            for i in range(B):
+                O.reset(cfg, oenvs[i], seed=int(seeds[i]) if r == 0 else None)
+            assert np.array_equal(goal, np.array([list(e.goal)[:4] for e in oenvs]))
+            assert np.allclose(np.linalg.norm(goal, axis=1), 1.0, atol=1e-12)
+        else:
+            assert np.array_equal(goal, golden[f"{task}_goal"][:, r])
+            assert np.array_equal(obs["desired_goal"].cpu().numpy(), golden[f"{task}_goal"][:, r].astype(np.float32))
+        if task == "stack":
+            pos = torch.cat([env.sim.get_base_position("object1"), env.sim.get_base_position("object2")], -1)
+        elif task != "reach":
+            pos = env.sim.get_base_position("object")
         if task != "reach":
-            cpos = env.sim.get_base_position("object").cpu().numpy()
-            assert np.array_equal(cpos, golden[f"{task}_object"][:, r].astype(np.float32))
+            assert np.array_equal(pos.cpu().numpy(), golden[f"{task}_object"][:, r].astype(np.float32))
 
 
 def test_compute_reward_goldens_bit_exact(ps, golden):
@@ -113,6 +132,20 @@ def test_compute_reward_goldens_bit_exact(ps, golden):
         her = env.compute_reward(torch.from_numpy(golden["her_ag"]).cuda(), torch.from_numpy(golden["her_dg"]).cuda())
         assert her.shape == (32, 32)
         assert np.array_equal(her.cpu().numpy().view(np.uint32), golden[f"her_reward_{reward_type}"].view(np.uint32))
+
+
+@pytest.mark.parametrize("task", ["stack", "flip"])
+def test_compute_reward_goldens_stack_flip(ps, golden, task):
+    """stack.py:118-131 (6-D distance, threshold 0.1) and flip.py:80-91
+    (1 - <q, g>^2, threshold 0.2) against the reference's functions."""
+    for reward_type in ["sparse", "dense"]:
+        env = make_env(ps, task, "ee", 8, reward=reward_type)
+        ag = torch.from_numpy(golden[f"{task}_ag"]).cuda()
+        dg = torch.from_numpy(golden[f"{task}_dg"]).cuda()
+        r = env.compute_reward(ag, dg, {}).cpu().numpy()
+        want = golden[f"{task}_reward_{reward_type}"]
+        assert np.array_equal(r.view(np.uint32), want.view(np.uint32))
+        assert np.array_equal(env.compute_success(ag, dg).cpu().numpy(), golden[f"{task}_success"])
 
 
 # ------------------------------------------------------------ physics parity
@@ -161,7 +194,14 @@ SIM_TIGHT = dict(q=2e-4, qd=5e-3)
 SIM_LOOSE = dict(q=1e-2, qd=1.0)
 
 
-@pytest.mark.parametrize("task", ["reach", "push", "pick_and_place"])
+def _object_rows(task):
+    return {"reach": [], "stack": [63, 76]}.get(task, [63])
+
+
+OBJ_ATOL = {"push": 5e-4, "slide": 5e-4}
+
+
+@pytest.mark.parametrize("task", ALL_TASKS)
 def test_sim_step_parity_same_motors(ps, task):
     """Engine step (20 substeps) from identical joints, motors and object."""
     B = 128
@@ -181,12 +221,13 @@ def test_sim_step_parity_same_motors(ps, task):
             O.sim_step(cfg, e)
             err_q.append(np.abs(after["f"][0:9, i] - np.array(e.q)).max())
             err_qd.append(np.abs(after["f"][9:18, i] - np.array(e.qd)).max())
-            if task != "reach":
-                assert np.allclose(after["f"][63:66, i], np.array(e.cpos), atol=5e-4 if task == "push" else 5e-3), (s, i)
+            for b, row in enumerate(_object_rows(task)):
+                assert np.allclose(after["f"][row:row + 3, i], np.array(e.obj[b].pos),
+                                   atol=OBJ_ATOL.get(task, 5e-3)), (s, i, b)
     err_q, err_qd = np.array(err_q), np.array(err_qd)
     tight = (err_q < SIM_TIGHT["q"]) & (err_qd < SIM_TIGHT["qd"])
     print(task, f"max q {err_q.max():.1e} qd {err_qd.max():.1e}; tight {tight.mean() * 100:.1f} % of {tight.size}")
-    if task == "pick_and_place":
+    if task in FREE_GRIPPER:
         assert tight.mean() >= 0.95
         assert err_q.max() < SIM_LOOSE["q"] and err_qd.max() < SIM_LOOSE["qd"]
     else:
@@ -199,23 +240,34 @@ def test_sim_step_parity_same_motors(ps, task):
 # ee position by 8e-4, ee velocity by 3e-2 and finger width by 3.4e-3 under
 # fp32-ulp-sized state perturbations (test_oracle.py::
 # test_pick_and_place_conditioning), so its bounds are ~3x that conditioning.
+_PNP = dict(ee_pos=3e-3, ee_vel=1e-1, width=1e-2, obj_pos=1e-3, obj_rot=5e-3, obj_vel=5e-2, obj_avel=2e-1)
 TOL = {
     "reach": dict(ee_pos=2e-5, ee_vel=2e-3),
     "push": dict(ee_pos=2e-5, ee_vel=2e-3, obj_pos=2e-5, obj_rot=1e-4, obj_vel=1e-4, obj_avel=2e-3),
-    "pick_and_place": dict(ee_pos=3e-3, ee_vel=1e-1, width=1e-2, obj_pos=1e-3, obj_rot=5e-3, obj_vel=5e-2,
-                           obj_avel=2e-1),
+    "slide": dict(ee_pos=2e-5, ee_vel=2e-3, obj_pos=2e-5, obj_rot=1e-4, obj_vel=1e-4, obj_avel=2e-3),
+    "pick_and_place": _PNP,
+    "stack": dict(_PNP, **{f"obj2_{k[4:]}": v for k, v in _PNP.items() if k.startswith("obj_")}),
+    "flip": _PNP,
 }
 
 
-def _groups(obs_dim):
+def _groups(task, robot_dim):
+    """Observation slices: robot (panda.py:109-119), then the task's object
+    blocks (position, rotation -- a quaternion for Flip --, velocity, angular
+    velocity; Stack has two)."""
     g = {"ee_pos": [0, 1, 2], "ee_vel": [3, 4, 5]}
-    k = 6
-    if obs_dim in (7, 19):
+    if robot_dim == 7:
         g["width"] = [6]
-        k = 7
-    if obs_dim > 7:
-        g.update(obj_pos=[k, k + 1, k + 2], obj_rot=[k + 3, k + 4, k + 5], obj_vel=[k + 6, k + 7, k + 8],
-                 obj_avel=[k + 9, k + 10, k + 11])
+    k = robot_dim
+    nrot = 4 if task == "flip" else 3
+    for b in range({"reach": 0, "stack": 2}.get(task, 1)):
+        p = "obj_" if b == 0 else "obj2_"
+        g[p + "pos"] = list(range(k, k + 3))
+        g[p + "rot"] = list(range(k + 3, k + 3 + nrot))
+        k += 3 + nrot
+        g[p + "vel"] = list(range(k, k + 3))
+        g[p + "avel"] = list(range(k + 3, k + 6))
+        k += 6
     return g
 
 
@@ -228,7 +280,8 @@ def test_env_step_parity_teacher_forced(ps, task, control):
     env.reset(seed=12345)
     cfg = oracle_config_for(env.sim.cfg)
     rng = np.random.default_rng(7)
-    groups = _groups(env.obs_dim)
+    groups = _groups(task, 7 if task in FREE_GRIPPER else 6)
+    assert max(max(v) for v in groups.values()) == env.obs_dim - 1
     worst = {k: 0.0 for k in groups}
     flag_mismatch = 0
     for s in range(steps):
@@ -268,7 +321,7 @@ def test_reach_free_running_parity(ps):
             assert np.allclose(og[i, 3:], o[3:], atol=2e-2), (s, i)
 
 
-@pytest.mark.parametrize("task", ["reach", "push", "pick_and_place"])
+@pytest.mark.parametrize("task", ALL_TASKS)
 def test_autoreset_continues_generator(ps, task):
     """Every in-kernel reset (success or TimeLimit) draws the next goal/object
     from the env's own PCG64 stream: after n resets the goal equals the
@@ -279,17 +332,18 @@ def test_autoreset_continues_generator(ps, task):
     cfg = oracle_config_for(env.sim.cfg)
     zeros = torch.zeros(B, env.action_dim, device="cuda")
     n_resets = np.zeros(B, int)
-    for s in range(60):
+    for s in range(env.max_episode_steps + 10):
         obs, r, te, tr, info = env.step(zeros)
         n_resets += (te | tr).cpu().numpy().astype(int)
     assert (n_resets >= 1).all()
-    goal = env.sim.goal[:, :B].t().cpu().numpy()
+    G = env.goal_dim
+    goal = env.sim.goal[:G, :B].t().cpu().numpy()
     for i in range(B):
         e = O.new_env(cfg)
         O.reset(cfg, e, seed=100 + i)
         for _ in range(n_resets[i]):
             O.reset(cfg, e, seed=None)
-        assert np.array_equal(goal[i], np.array(e.goal))
+        assert np.array_equal(goal[i], np.array(e.goal)[:G])
 
 
 def test_determinism_and_save_restore(ps):
@@ -317,7 +371,7 @@ def test_determinism_and_save_restore(ps):
         env.restore_state(sid)
 
 
-@pytest.mark.parametrize("task", ["push", "pick_and_place"])
+@pytest.mark.parametrize("task", OBJECT_TASKS)
 def test_large_batch_properties(ps, task):
     """At the bench size: finite, bounded observations and exact TimeLimit."""
     B = 65536
@@ -330,6 +384,7 @@ def test_large_batch_properties(ps, task):
     # a gripper strike can spin the 4 cm cube to tens of rad/s (the oracle
     # reproduces these states: DESIGN.md §Parity); everything stays physical
     assert (o.abs() < 100).all()
-    assert (env.sim.get_base_position("object")[:, 2] > -0.45).all()
+    for body in (("object1", "object2") if task == "stack" else ("object",)):
+        assert (env.sim.get_base_position(body)[:, 2] > -0.45).all()
     assert not tr.any()
     assert int(env.sim.elapsed[:B].max()) <= 5 and int(env.sim.elapsed[:B].min()) >= 0

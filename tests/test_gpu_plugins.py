@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 import torch
 
-from test_gpu_parity import TOL, _groups
+from test_gpu_parity import FREE_GRIPPER, TOL, _groups
 
 pytestmark = pytest.mark.gpu
 
@@ -24,27 +24,42 @@ def ps():
     return pandasim
 
 
-ENV_IDS = {"reach": "PandaReach", "push": "PandaPush", "pick_and_place": "PandaPickAndPlace"}
+ENV_IDS = {"reach": "PandaReach", "push": "PandaPush", "pick_and_place": "PandaPickAndPlace",
+           "slide": "PandaSlide", "stack": "PandaStack", "flip": "PandaFlip"}
 
 
-@pytest.mark.parametrize("task", ["reach", "push", "pick_and_place"])
+@pytest.mark.parametrize("task", list(ENV_IDS))
 def test_plugin_reset_goldens_bit_exact(ps, golden, task):
     seeds = golden["seeds"]
-    env = ps.make(f"{ENV_IDS[task]}-v3", num_envs=len(seeds), fused=False)
-    for r in range(golden[f"{task}_goal"].shape[1]):
+    B = len(seeds)
+    env = ps.make(f"{ENV_IDS[task]}-v3", num_envs=B, fused=False)
+    fused = ps.make(f"{ENV_IDS[task]}-v3", num_envs=B) if task == "flip" else None
+    for r in range(golden[f"{task}_object"].shape[1]):
         obs, info = env.reset(seed=seeds if r == 0 else None)
         assert env.task.goal.dtype == torch.float64
-        assert np.array_equal(env.task.get_goal().cpu().numpy(), golden[f"{task}_goal"][:, r])
-        assert np.array_equal(obs["desired_goal"].cpu().numpy(), golden[f"{task}_goal"][:, r].astype(np.float32))
-        if task != "reach":
-            cpos = env.sim.get_base_position("object").cpu().numpy()
-            assert np.array_equal(cpos, golden[f"{task}_object"][:, r].astype(np.float32))
+        goal = env.task.get_goal().cpu().numpy()
+        if task == "flip":  # unseeded Rotation.random() in the reference: the fused kernel's aux stream
+            fused.reset(seed=seeds if r == 0 else None)
+            assert np.array_equal(goal, fused.sim.goal[:4, :B].t().cpu().numpy())
+            assert np.array_equal(env.sim.get_base_orientation("target").cpu().numpy(), goal)
+        else:
+            assert np.array_equal(goal, golden[f"{task}_goal"][:, r])
+            assert np.array_equal(obs["desired_goal"].cpu().numpy(), golden[f"{task}_goal"][:, r].astype(np.float32))
+        bodies = {"reach": [], "stack": ["object1", "object2"]}.get(task, ["object"])
+        if bodies:
+            pos = torch.cat([env.sim.get_base_position(b) for b in bodies], -1).cpu().numpy()
+            assert np.array_equal(pos, golden[f"{task}_object"][:, r].astype(np.float32))
+        if task == "stack":
+            for b, sl in (("target1", slice(0, 3)), ("target2", slice(3, 6))):
+                assert np.array_equal(env.sim.get_base_position(b).cpu().numpy(), golden["stack_goal"][:, r, sl])
+        elif task not in ("reach", "flip"):
             tpos = env.sim.get_base_position("target").cpu().numpy()
             assert np.array_equal(tpos, golden[f"{task}_goal"][:, r])
 
 
 @pytest.mark.parametrize("task,control", [("reach", "ee"), ("reach", "joints"), ("push", "ee"),
-                                          ("pick_and_place", "ee"), ("pick_and_place", "joints")])
+                                          ("pick_and_place", "ee"), ("pick_and_place", "joints"), ("slide", "ee"),
+                                          ("stack", "ee"), ("stack", "joints"), ("flip", "ee")])
 def test_plugin_path_matches_fused_kernel(ps, task, control):
     """Teacher-forced: from the fused env's state, one plugin-path step and one
     fused step agree within the fused-vs-oracle tolerances."""
@@ -55,9 +70,9 @@ def test_plugin_path_matches_fused_kernel(ps, task, control):
     fused.reset(seed=777)
     env = ps.make(f"{ENV_IDS[task]}{'Joints' if control == 'joints' else ''}Dense-v3", num_envs=B, fused=False)
     env.reset(seed=777)
-    assert torch.equal(env.task.get_goal(), fused.sim.goal[:, :B].t())
+    assert torch.equal(env.task.get_goal(), fused.sim.goal[:fused.goal_dim, :B].t())
     rng = np.random.default_rng(17)
-    groups = _groups(fused.obs_dim)
+    groups = _groups(task, 7 if task in FREE_GRIPPER else 6)
     worst = {k: 0.0 for k in groups}
     for s in range(8):
         env.sim.state.copy_(fused.sim.state)
@@ -69,7 +84,8 @@ def test_plugin_path_matches_fused_kernel(ps, task, control):
         for k, idx in groups.items():
             worst[k] = max(worst[k], float((o_p["observation"][:, idx] - o_f["observation"][:, idx]).abs().max()))
         # dense reward = -distance: agrees to the achieved-goal tolerance
-        assert float((r_p - r_f).abs().max()) <= 2 * TOL[task]["ee_pos" if task == "reach" else "obj_pos"]
+        ag_tol = TOL[task]["ee_pos" if task == "reach" else "obj_rot" if task == "flip" else "obj_pos"]
+        assert float((r_p - r_f).abs().max()) <= 4 * ag_tol
         assert int((te_p != te_f.bool()).sum()) <= 2
         assert torch.equal(info["is_success"], te_p)
         assert not tr_p.any()
@@ -124,7 +140,9 @@ def test_plugin_goal_required_and_scene_validation(ps):
     with pytest.raises(RuntimeError):
         task.get_goal()  # core.py:185-186
     with pytest.raises(NotImplementedError):
-        sim.create_table(length=2.0, width=0.7, height=0.4, x_offset=-0.3)
+        sim.create_table(length=2.0, width=0.7, height=0.4, x_offset=-0.3, lateral_friction=0.3)
+    with pytest.raises(NotImplementedError):
+        sim.create_box(body_name="slab", half_extents=[0.1, 0.02, 0.02], mass=1.0, position=[0, 0, 0.02])
     with pytest.raises(NotImplementedError):
         sim.loadURDF("ur5", "ur5/ur5.urdf", useFixedBase=True)
     with pytest.raises(ValueError):

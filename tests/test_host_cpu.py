@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from pandasim.core import TimeLimit, np_random
-from pandasim.tasks import PickAndPlace, Push, Reach
+from pandasim.tasks import Flip, PickAndPlace, Push, Reach, Slide, Stack
 from pandasim.utils import angle_distance, distance
 
 
@@ -37,30 +37,62 @@ class FakeSim:
     def uniform(self, low, high):
         return torch.from_numpy(np.stack([g.uniform(low, high) for g in self.gens]))
 
+    def random_rotation(self):
+        return torch.tensor([[0.0, 0.0, 0.0, 1.0]] * self.num_envs, dtype=torch.float64)
+
     def set_base_pose(self, body, position, orientation):
         self.poses[body] = torch.as_tensor(position).clone()
+        self.orns = getattr(self, "orns", {})
+        self.orns[body] = torch.as_tensor(np.asarray(orientation) if not torch.is_tensor(orientation)
+                                          else orientation).clone()
 
     def get_base_position(self, body):
         return self.poses[body].to(torch.float32)
 
 
-@pytest.mark.parametrize("task", ["reach", "push", "pick_and_place"])
+CLASSES = {"push": Push, "pick_and_place": PickAndPlace, "slide": Slide, "stack": Stack, "flip": Flip}
+
+
+@pytest.mark.parametrize("task", ["reach", "push", "pick_and_place", "slide", "stack", "flip"])
 def test_task_reset_draw_order_matches_goldens(golden, task):
     seeds = golden["seeds"]
     sim = FakeSim(len(seeds))
     if task == "reach":
         t = Reach(sim, get_ee_position=lambda: torch.zeros(len(seeds), 3))
     else:
-        t = (Push if task == "push" else PickAndPlace)(sim)
+        t = CLASSES[task](sim)
     assert "create_table" in sim.calls and "create_plane" in sim.calls
-    for r in range(golden[f"{task}_goal"].shape[1]):
+    for r in range(golden[f"{task}_object"].shape[1]):
         if r == 0:
             t.np_random, _ = np_random(sim, seeds)
         t.reset()
-        assert np.array_equal(t.get_goal().numpy(), golden[f"{task}_goal"][:, r])
-        assert np.array_equal(sim.poses["target"].numpy(), golden[f"{task}_goal"][:, r])
+        if task == "flip":
+            assert np.array_equal(sim.orns["target"].numpy(), t.get_goal().numpy())
+            assert np.array_equal(sim.orns["object"], np.zeros(3))  # flip.py:77: Euler zeros
+        elif task == "stack":
+            assert np.array_equal(t.get_goal().numpy(), golden["stack_goal"][:, r])
+            assert np.array_equal(sim.poses["target1"].numpy(), golden["stack_goal"][:, r, :3])
+            assert np.array_equal(sim.poses["target2"].numpy(), golden["stack_goal"][:, r, 3:])
+            got = np.concatenate([sim.poses["object1"].numpy(), sim.poses["object2"].numpy()], -1)
+            assert np.array_equal(got, golden["stack_object"][:, r])
+            continue
+        else:
+            assert np.array_equal(t.get_goal().numpy(), golden[f"{task}_goal"][:, r])
+            assert np.array_equal(sim.poses["target"].numpy(), golden[f"{task}_goal"][:, r])
         if task != "reach":
             assert np.array_equal(sim.poses["object"].numpy(), golden[f"{task}_object"][:, r])
+
+
+@pytest.mark.parametrize("task", ["stack", "flip"])
+def test_stack_flip_reward_success_goldens_host(golden, task):
+    """The host fallback of goal_reward_and_success (CPU tensors): Stack's
+    6-D distance and Flip's 1 - <q, g>^2 against the reference's functions."""
+    ag, dg = torch.from_numpy(golden[f"{task}_ag"]), torch.from_numpy(golden[f"{task}_dg"])
+    for rt in ("sparse", "dense"):
+        t = CLASSES[task](FakeSim(1), reward_type=rt)
+        r = t.compute_reward(ag, dg, {}).numpy()
+        assert np.array_equal(r.view(np.uint32), golden[f"{task}_reward_{rt}"].view(np.uint32)), rt
+        assert np.array_equal(t.is_success(ag, dg).numpy(), golden[f"{task}_success"])
 
 
 def test_distance_reward_success_goldens(golden):

@@ -16,7 +16,7 @@ import pytest
 
 def kat_config():
     # PyBullet() + loadURDF("franka_panda/panda.urdf", basePosition=0, useFixedBase=True), no other bodies
-    return O.config("reach", base=(0.0, 0.0, 0.0), has_table=0, has_plane=0, has_cube=0)
+    return O.config("reach", base=(0.0, 0.0, 0.0), has_table=0, has_plane=0, n_objects=0)
 
 
 def test_dt():  # pybullet_test.py:30-35
@@ -70,16 +70,17 @@ def test_inverse_kinematics():  # pybullet_test.py:254-266
 
 
 def test_box_free_fall_velocity():  # pybullet_test.py:56-64 (1 kg box, half extents 0.5, one step())
-    cfg = O.config("push", base=(0, 0, 0), has_table=0, has_plane=0, has_robot=0, cube_half=0.5, cube_mass=1.0)
+    cfg = O.config("push", base=(0, 0, 0), has_table=0, has_plane=0, has_robot=0, object_half=(0.5, 0.5, 0.5),
+                   object_mass=1.0)
     env = O.new_env(cfg)
     O.sim_step(cfg, env)
-    assert np.allclose(np.array(env.cvel), [0.0, 0.0, -0.392], atol=1e-3)
-    assert np.allclose(np.array(env.comg), 0.0, atol=1e-3)  # :89-97
+    assert np.allclose(np.array(env.obj[0].vel), [0.0, 0.0, -0.392], atol=1e-3)
+    assert np.allclose(np.array(env.obj[0].omg), 0.0, atol=1e-3)  # :89-97
     e = np.zeros(3)
-    O.lib().po_euler_from_quaternion(np.array(env.cquat).ctypes.data_as(O.C.POINTER(O.C.c_double)),
+    O.lib().po_euler_from_quaternion(np.array(env.obj[0].quat).ctypes.data_as(O.C.POINTER(O.C.c_double)),
                                      e.ctypes.data_as(O.C.POINTER(O.C.c_double)))
     assert np.allclose(e, 0.0, atol=1e-3)  # :78-86
-    assert np.allclose(np.array(env.cquat), [0, 0, 0, 1], atol=1e-3)  # :67-75
+    assert np.allclose(np.array(env.obj[0].quat), [0, 0, 0, 1], atol=1e-3)  # :67-75
 
 
 def test_set_joint_angles_roundtrip():  # pybullet_test.py:221-251
@@ -123,16 +124,46 @@ def test_pcg64_matches_numpy(seed):
     assert [O.pcg64_next(st) for _ in range(16)] == [int(bg.random_raw()) for _ in range(16)]
 
 
-@pytest.mark.parametrize("task", ["reach", "push", "pick_and_place"])
+@pytest.mark.parametrize("task", ["reach", "push", "pick_and_place", "slide", "stack", "flip"])
 def test_goal_sampling_golden(task, golden):
     cfg = O.config(task)
     for i, s in enumerate(golden["seeds"]):
         env = O.new_env(cfg)
-        for r in range(golden[f"{task}_goal"].shape[1]):
+        for r in range(golden[f"{task}_object"].shape[1]):
             O.reset(cfg, env, seed=int(s) if r == 0 else None)
-            assert np.array_equal(np.array(env.goal), golden[f"{task}_goal"][i, r])
-            if task != "reach":
-                assert np.array_equal(np.array(env.cpos), golden[f"{task}_object"][i, r])
+            if task != "flip":  # Flip's goal is not seeded in the reference (flip.py:70-72)
+                assert np.array_equal(np.array(env.goal)[:O.goal_dim(cfg)], golden[f"{task}_goal"][i, r])
+            if task == "stack":
+                assert np.array_equal(np.array(env.obj[0].pos), golden["stack_object"][i, r, :3])
+                assert np.array_equal(np.array(env.obj[1].pos), golden["stack_object"][i, r, 3:])
+            elif task != "reach":
+                assert np.array_equal(np.array(env.obj[0].pos), golden[f"{task}_object"][i, r])
+
+
+def test_flip_goal_is_a_unit_quaternion_stream():
+    cfg = O.config("flip")
+    env = O.new_env(cfg)
+    goals = []
+    for r in range(400):
+        O.reset(cfg, env, seed=77 if r == 0 else None)
+        goals.append(np.array(env.goal[:4]))
+    g = np.array(goals)
+    assert np.allclose(np.linalg.norm(g, axis=1), 1.0)
+    # uniform over rotations: E[q_i^2] = 1/4, components symmetric
+    assert np.allclose((g ** 2).mean(0), 0.25, atol=0.05) and np.allclose(g.mean(0), 0.0, atol=0.1)
+    env2 = O.new_env(cfg)
+    O.reset(cfg, env2, seed=77)
+    assert np.array_equal(np.array(env2.goal[:4]), g[0])  # seeded: reproducible
+
+
+@pytest.mark.parametrize("task", ["stack", "flip"])
+def test_stack_flip_reward_goldens(task, golden):
+    ag, dg = golden[f"{task}_ag"], golden[f"{task}_dg"]
+    for rt in ("sparse", "dense"):
+        r = np.array([O.compute_reward(rt, a, d, task=task) for a, d in zip(ag, dg)], np.float32)
+        assert np.array_equal(r.view(np.uint32), golden[f"{task}_reward_{rt}"].view(np.uint32)), rt
+    su = np.array([O.is_success(a, d, task=task) for a, d in zip(ag, dg)])
+    assert np.array_equal(su, golden[f"{task}_success"])
 
 
 def test_reward_and_success_golden(golden):
