@@ -1255,9 +1255,13 @@ static double uniform(uint64_t rng[4], double lo, double hi) {
 /* Flip's goal: scipy Rotation.random() (flip.py:70-72) draws from numpy's
  * unseeded global RandomState, so no seed of the reference reproduces it.
  * Here it comes from a per-env splitmix64 stream (seeded with the env seed,
- * separate from np_random so the object draws stay the reference's):
- * four Box-Muller normals, normalised -- the same uniform distribution over
- * rotations as R.random(). */
+ * separate from np_random so the object draws stay the reference's), mapped
+ * to a unit quaternion by Marsaglia's method (Ann. Math. Stat. 43, 1972):
+ * (x1, x2) and (x3, x4) uniform in the unit disc by rejection, then
+ * q = (x1, x2, x3 t, x4 t) with t = sqrt((1 - s1) / s2) -- uniform on S^3,
+ * i.e. the same uniform distribution over rotations as R.random().  Only
+ * +, *, / and sqrt are used, all correctly rounded, so the HIP kernel
+ * (ps_task.h random_rotation) reproduces it bit for bit. */
 static uint64_t splitmix64(uint64_t *st) {
     uint64_t z = (*st += 0x9E3779B97F4A7C15ULL);
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -1267,17 +1271,30 @@ static uint64_t splitmix64(uint64_t *st) {
 
 static uint64_t aux_seed(uint64_t seed) { return seed ^ 0x5851F42D4C957F2DULL; }
 
-void po_flip_goal(uint64_t *aux_state, double quat[4]) {
-    double nrm[4];
-    for (int k = 0; k < 2; k++) {
-        double u1 = (double)(splitmix64(aux_state) >> 11) * (1.0 / 9007199254740992.0);
-        double u2 = (double)(splitmix64(aux_state) >> 11) * (1.0 / 9007199254740992.0);
-        double rad = sqrt(-2.0 * log(1.0 - u1)), th = 2.0 * 3.14159265358979323846 * u2;
-        nrm[2 * k] = rad * cos(th);
-        nrm[2 * k + 1] = rad * sin(th);
+/* uniform in (-1, 1): 53 random bits */
+static double aux_signed_unit(uint64_t *st) {
+    return (double)(splitmix64(st) >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+}
+
+static double disc_point(uint64_t *st, double *x, double *y) {
+    for (;;) {
+        *x = aux_signed_unit(st);
+        *y = aux_signed_unit(st);
+        double a = *x * *x, b = *y * *y;
+        double s = a + b;
+        if (s < 1.0 && s > 0.0) return s;
     }
-    double n = sqrt(nrm[0] * nrm[0] + nrm[1] * nrm[1] + nrm[2] * nrm[2] + nrm[3] * nrm[3]);
-    for (int d = 0; d < 4; d++) quat[d] = nrm[d] / n;
+}
+
+void po_flip_goal(uint64_t *aux_state, double quat[4]) {
+    double x1, x2, x3, x4;
+    double s1 = disc_point(aux_state, &x1, &x2);
+    double s2 = disc_point(aux_state, &x3, &x4);
+    double t = sqrt((1.0 - s1) / s2);
+    quat[0] = x1;
+    quat[1] = x2;
+    quat[2] = x3 * t;
+    quat[3] = x4 * t;
 }
 
 /* panda_tasks.py:14-113 wiring + each task's _create_scene */

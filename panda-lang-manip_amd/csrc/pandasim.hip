@@ -291,8 +291,11 @@ PS_D float reward_for(int reward_type, double d, double thr) {
     return -__double2float_rn(d);
 }
 
-// splitmix64 stream of Flip's goal (oracle po_flip_goal): R.random() as four
-// Box-Muller normals, normalised (flip.py:70-72)
+// splitmix64 stream of Flip's goal (oracle po_flip_goal): R.random()
+// (flip.py:70-72) as a uniform unit quaternion by Marsaglia's method -- two
+// rejection-sampled points of the unit disc, q = (x1, x2, x3 t, x4 t),
+// t = sqrt((1 - s1) / s2).  Only correctly rounded +, *, / and sqrt, kept
+// uncontracted, so the oracle's draws are reproduced bit for bit.
 PS_D uint64_t splitmix64(uint64_t &st) {
     uint64_t z = (st += 0x9E3779B97F4A7C15ULL);
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -300,19 +303,29 @@ PS_D uint64_t splitmix64(uint64_t &st) {
     return z ^ (z >> 31);
 }
 PS_D uint64_t aux_seed(uint64_t seed) { return seed ^ 0x5851F42D4C957F2DULL; }
-PS_D void random_rotation(uint64_t &st, double q[4]) {
-    double nrm[4];
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        double u1 = (double)(splitmix64(st) >> 11) * (1.0 / 9007199254740992.0);
-        double u2 = (double)(splitmix64(st) >> 11) * (1.0 / 9007199254740992.0);
-        double rad = sqrt(-2.0 * log(1.0 - u1)), th = 2.0 * 3.14159265358979323846 * u2;
-        nrm[2 * k] = rad * cos(th);
-        nrm[2 * k + 1] = rad * sin(th);
+PS_D double aux_signed_unit(uint64_t &st) {
+#pragma clang fp contract(off)
+    return __dsub_rn(opaque(__dmul_rn((double)(splitmix64(st) >> 11), 2.0 / 9007199254740992.0)), 1.0);
+}
+PS_D double disc_point(uint64_t &st, double &x, double &y) {
+#pragma clang fp contract(off)
+    for (;;) {
+        x = aux_signed_unit(st);
+        y = aux_signed_unit(st);
+        double s = __dadd_rn(opaque(__dmul_rn(x, x)), opaque(__dmul_rn(y, y)));
+        if (s < 1.0 && s > 0.0) return s;
     }
-    double n = sqrt(nrm[0] * nrm[0] + nrm[1] * nrm[1] + nrm[2] * nrm[2] + nrm[3] * nrm[3]);
-#pragma unroll
-    for (int d = 0; d < 4; d++) q[d] = nrm[d] / n;
+}
+PS_D void random_rotation(uint64_t &st, double q[4]) {
+#pragma clang fp contract(off)
+    double x1, x2, x3, x4;
+    double s1 = disc_point(st, x1, x2);
+    double s2 = disc_point(st, x3, x4);
+    double t = __dsqrt_rn(__ddiv_rn(__dsub_rn(1.0, s1), s2));
+    q[0] = x1;
+    q[1] = x2;
+    q[2] = __dmul_rn(x3, t);
+    q[3] = __dmul_rn(x4, t);
 }
 
 PS_D void place(Body &b, double x, double y, double z) {

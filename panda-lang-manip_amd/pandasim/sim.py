@@ -14,6 +14,7 @@ import itertools
 import math
 from typing import Dict, Optional, Sequence
 
+import numpy as np
 import torch
 
 from . import _lib as L
@@ -191,8 +192,9 @@ class PandaSim:
         fric = 0.5 if lateral_friction is None else float(lateral_friction)
         if n >= 2 or mass <= 0:
             raise NotImplementedError("at most two dynamic objects (Stack) are compiled in")
-        if n == 1 and (shape != self.cfg.object_shape or [float(h) for h in half] != list(self.cfg.object_half)
-                       or fric != self.cfg.object_friction or shape != L.SHAPE_BOX):
+        f32 = lambda v: [float(np.float32(x)) for x in v]  # the config holds float32
+        if n == 1 and (shape != self.cfg.object_shape or f32(half) != list(self.cfg.object_half)
+                       or f32([fric]) != [self.cfg.object_friction] or shape != L.SHAPE_BOX):
             raise NotImplementedError("a second object must be a cube like the first (Stack)")
         if shape == L.SHAPE_BOX and max(half) != min(half):
             raise NotImplementedError("boxes must be cubes (isotropic inertia)")
