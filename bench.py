@@ -36,40 +36,63 @@ def algorithmic_bytes_per_env_step(obs_dim: int, action_dim: int, goal_dim: int 
     return read + write
 
 
+def host_threads() -> int:
+    """Host threads this process may use: the affinity mask, capped by
+    OMP_NUM_THREADS (16 on the GPU box, whose nproc shows the whole machine)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
 def cpu_baseline(task: str, seconds: float):
-    """The oracle (fp64 C restatement, 1 thread) on a bounded sample of the same workload."""
+    """The oracle (fp64 C restatement) on a bounded sample of the same workload:
+    a third of the time on 1 host thread, the rest on every host thread this
+    process may use (OpenMP over envs, oracle/panda_oracle.c po_step_batch).
+    `value`/`cores` are the all-threads figure; `value_1core` the scalar one."""
     import numpy as np
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
     cfg = O.config(task)
-    n_env = 64
-    envs = (O.Env * n_env)()
-    for i in range(n_env):
-        O.lib().po_init_env(O.C.byref(cfg), O.C.byref(envs[i]))
-        O.lib().po_reset(O.C.byref(cfg), O.C.byref(envs[i]), 1, 12345 + i, None, None, None)
+    threads = host_threads()
     na, od = O.action_dim(cfg), O.obs_dim(cfg)
-    rng = np.random.default_rng(0xC0FFEE)
-    obs = np.zeros((n_env, od), np.float32)
-    ag = np.zeros((n_env, 3), np.float32)
-    dg = np.zeros((n_env, 3), np.float32)
-    rew = np.zeros(n_env, np.float32)
-    te = np.zeros(n_env, np.uint8)
-    tr = np.zeros(n_env, np.uint8)
     fp = lambda a: a.ctypes.data_as(O.C.POINTER(O.C.c_float))
     u8 = lambda a: a.ctypes.data_as(O.C.POINTER(O.C.c_uint8))
-    steps = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        a = rng.uniform(-1, 1, size=(n_env, na)).astype(np.float32)
-        O.lib().po_step_batch(O.C.byref(cfg), envs, n_env, fp(a), fp(obs), fp(ag), fp(dg), fp(rew), u8(te), u8(tr), 1,
-                              None)
-        steps += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(n_env * steps / dt, 2), "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n_env} envs x {steps} steps of {task} (ee, sparse) in {dt:.1f} s on 1 host thread "
-                      f"(fp64 oracle; PyBullet not installed)"}
+
+    def run(n_threads, n_env, budget):
+        used = O.lib().po_set_threads(n_threads)
+        envs = (O.Env * n_env)()
+        for i in range(n_env):
+            O.lib().po_init_env(O.C.byref(cfg), O.C.byref(envs[i]))
+            O.lib().po_reset(O.C.byref(cfg), O.C.byref(envs[i]), 1, 12345 + i, None, None, None)
+        rng = np.random.default_rng(0xC0FFEE)
+        obs = np.zeros((n_env, od), np.float32)
+        ag = np.zeros((n_env, 3), np.float32)
+        dg = np.zeros((n_env, 3), np.float32)
+        rew = np.zeros(n_env, np.float32)
+        te = np.zeros(n_env, np.uint8)
+        tr = np.zeros(n_env, np.uint8)
+        steps = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < budget:
+            a = rng.uniform(-1, 1, size=(n_env, na)).astype(np.float32)
+            O.lib().po_step_batch(O.C.byref(cfg), envs, n_env, fp(a), fp(obs), fp(ag), fp(dg), fp(rew), u8(te),
+                                  u8(tr), 1, None)
+            steps += 1
+        dt = time.perf_counter() - t0
+        return n_env * steps / dt, used, steps, dt
+
+    v1, _, s1, d1 = run(1, 64, seconds / 3)
+    n_env = 16 * threads
+    vn, used, sn, dn = run(threads, n_env, seconds * 2 / 3)
+    return {"value": round(vn, 2), "unit": "env-steps/s", "cores": used, "kind": "port",
+            "value_1core": round(v1, 2),
+            "sample": f"{n_env} envs x {sn} steps of {task} (ee, sparse) in {dn:.1f} s on {used} host threads "
+                      f"(OpenMP over envs) + 64 envs x {s1} steps in {d1:.1f} s on 1 thread; fp64 oracle, "
+                      f"PyBullet not installed on the box"}
 
 
 def load_pmc_traffic(workload: str):

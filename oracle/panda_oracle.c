@@ -1564,10 +1564,28 @@ void po_step(const po_config *cfg, po_env *env, const float *action, float *obs,
     }
 }
 
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* Threads po_step_batch may use (OpenMP over envs); returns the count in effect. */
+int po_set_threads(int n) {
+#ifdef _OPENMP
+    if (n > 0) omp_set_num_threads(n);
+    return omp_get_max_threads();
+#else
+    (void)n;
+    return 1;
+#endif
+}
+
 void po_step_batch(const po_config *cfg, po_env *envs, int n, const float *actions, float *obs, float *ag,
                    float *dg, float *reward, uint8_t *terminated, uint8_t *truncated, int autoreset,
                    po_stats *stats) {
     int na = po_action_dim(cfg), od = po_obs_dim(cfg), gd = po_goal_dim(cfg);
+    model_init(); /* before the threads: the model tables are built lazily */
+    /* envs are independent; stats (shared counters) forces the serial loop */
+#pragma omp parallel for schedule(dynamic, 4) if (stats == NULL)
     for (int i = 0; i < n; i++)
         po_step(cfg, &envs[i], actions + (size_t)i * na, obs + (size_t)i * od, ag + (size_t)i * gd,
                 dg + (size_t)i * gd, reward + i, terminated + i, truncated + i, autoreset, NULL, NULL, stats);

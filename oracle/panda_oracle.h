@@ -92,6 +92,7 @@ void po_get_obs(const po_config *cfg, const po_env *env, float *obs, float *ag, 
 void po_step(const po_config *cfg, po_env *env, const float *action, float *obs, float *ag, float *dg,
              float *reward, uint8_t *terminated, uint8_t *truncated, int autoreset, float *final_obs,
              float *final_ag, po_stats *stats);
+int po_set_threads(int n);
 void po_step_batch(const po_config *cfg, po_env *envs, int n, const float *actions, float *obs, float *ag,
                    float *dg, float *reward, uint8_t *terminated, uint8_t *truncated, int autoreset,
                    po_stats *stats);
