@@ -80,6 +80,8 @@ def lib():
         L.po_get_obs.argtypes = [P(Config), P(Env), F, F, F]
         L.po_step.argtypes = [P(Config), P(Env), F, F, F, F, F, U8, U8, I, F, F, P(Stats)]
         L.po_step_batch.argtypes = [P(Config), P(Env), I, F, F, F, F, F, U8, U8, I, P(Stats)]
+        L.po_set_threads.argtypes = [I]
+        L.po_set_threads.restype = I
         L.po_compute_reward.argtypes = [I, I, F, P(D)]
         L.po_compute_reward.restype = C.c_float
         L.po_is_success.argtypes = [I, F, P(D)]

@@ -999,7 +999,7 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
         }
     }
 
-    static orow rows[MAX_ROWS];
+    orow rows[MAX_ROWS]; /* per call: po_step_batch runs envs on several threads */
     int nr = 0;
     /* deep joint-limit violations are solved in split-impulse mode: the
      * velocity row only stops further violation and the position error is

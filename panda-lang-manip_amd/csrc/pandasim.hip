@@ -853,6 +853,14 @@ int ps_reset(ps_ctx *c, void *state, const uint8_t *mask, const uint64_t *seeds,
     return check_launch(c);
 }
 
+// PS_ISA_TASK (diagnostic builds only): instantiate the step kernels of one
+// task, so its ISA can be inspected without compiling all twelve
+#ifdef PS_ISA_TASK
+#define PS_TASK_ON(T) ((T) == PS_ISA_TASK)
+#else
+#define PS_TASK_ON(T) true
+#endif
+
 int ps_step(ps_ctx *c, void *state, const float *actions, float *obs, float *ag, float *dg, float *reward,
             uint8_t *terminated, uint8_t *truncated, int autoreset, float *final_obs, float *final_ag,
             void *stream) {
@@ -864,8 +872,11 @@ int ps_step(ps_ctx *c, void *state, const float *actions, float *obs, float *ag,
     dim3 g = grid_of(P.n, kBlock), b(kBlock);
     hipStream_t st = (hipStream_t)stream;
 #define PS_LAUNCH_STEP(T, C)                                                                                     \
-    hipLaunchKernelGGL((k_step<T, C>), g, b, 0, st, P, actions, obs, ag, dg, reward, terminated, truncated, \
-                       final_obs, final_ag)
+    do {                                                                                                         \
+        if constexpr (PS_TASK_ON(T))                                                                             \
+            hipLaunchKernelGGL((k_step<T, C>), g, b, 0, st, P, actions, obs, ag, dg, reward, terminated,        \
+                               truncated, final_obs, final_ag);                                                  \
+    } while (0)
 #define PS_LAUNCH_TASK(T)                                                  \
     if (c->cfg.control == PS_CONTROL_EE) PS_LAUNCH_STEP(T, PS_CONTROL_EE); \
     else PS_LAUNCH_STEP(T, PS_CONTROL_JOINTS);

@@ -53,6 +53,8 @@ PS_HD V3 operator*(float s, V3 a) { return V3{a.x * s, a.y * s, a.z * s}; }
 PS_HD float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 PS_HD V3 cross(V3 a, V3 b) { return V3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
 PS_D float norm(V3 a) { return sqrtf(dot(a, a)); }
+// c + a * s with one fma per component
+PS_HD V3 fma3(V3 a, float s, V3 c) { return V3{fmaf(a.x, s, c.x), fmaf(a.y, s, c.y), fmaf(a.z, s, c.z)}; }
 
 // row-major 3x3
 struct M3 {

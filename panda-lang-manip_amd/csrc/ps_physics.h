@@ -732,6 +732,14 @@ PS_D int box_box(const Scene &sc, const Body &b0, const Body &b1, const M3 &R0, 
 // fmaxf() in the residual max ignores, matching the reference's skip.
 PS_D float res_scale(float dinv) { return __builtin_amdgcn_rcpf(dinv); }
 
+// Friction-cone projection factor (resolveConeFrictionConstraintRows): lim/|f|
+// when |f|^2 = m2 exceeds lim^2, else 1.  Raw v_rsq_f32: rsqrtf's denormal
+// rescaling costs three instructions per cone row; m2 is clamped to FLT_MIN
+// instead, so a denormal m2 cannot produce inf (and 0 * inf) there.
+PS_D float cone_scale(float m2, float lim) {
+    return m2 > lim * lim ? lim * __builtin_amdgcn_rsqf(fmaxf(m2, 1.17549435e-38f)) : 1.0f;
+}
+
 // STD_MOTORS: the motors are the ones RobotTaskEnv.step sets (POSITION_CONTROL
 // on all nine joints with the fixed Panda gains and forces, panda.py:40-56), so
 // only the targets are per-env; otherwise every gain comes from `mt`.
@@ -1145,8 +1153,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             for (int c = 0; c < NG; c++)
                 if (__builtin_amdgcn_ballot_w64(c < ng[b])) {
                     GroundContact &g = gc[b][c];
-                    V3 rn = mk(g.r.y, -g.r.x, 0.0f);  // r x (0,0,1)
-                    float dl = g.rhs[0] - g.dinv[0] * (dot(rn, dw[b]) + dvl[b].z);
+                    V3 rn = mk(g.r.y, -g.r.x, 0.0f);  // r x (0,0,1); zero terms dropped below
+                    float dl = g.rhs[0] - g.dinv[0] * (rn.x * dw[b].x + rn.y * dw[b].y + dvl[b].z);
                     float nl = fminf(fmaxf(g.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
                     dl = nl - g.lam[0];
                     g.lam[0] = nl;
@@ -1184,6 +1192,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         for (int c = 0; c < NR; c++)
             if (__builtin_amdgcn_ballot_w64(c < nr)) {
                 RobotContact &r = rc[c];
+                // M^-1 J^T column first: its LDS latency hides under the dot
+                float mj[9];
+#pragma unroll
+                for (int a = 0; a < 9; a++) mj[a] = L.at(c, 0, a);
+                __builtin_amdgcn_sched_barrier(0);
                 float jv = jrow_dot(r.J[0], dv);
                 if (NOBJ > 0) jv -= dot(r.rn[0], obj_dw(r.o1)) + dot(r.dir[0], obj_dv(r.o1));
                 float dl = r.rhs[0] - r.dinv[0] * jv;
@@ -1191,11 +1204,15 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 dl = nl - r.lam[0];
                 r.lam[0] = nl;
 #pragma unroll
-                for (int a = 0; a < 9; a++) dv[a] = fmaf(L.at(c, 0, a), dl, dv[a]);
-                if constexpr (NOBJ > 0) {
-                    float im = NOBJ == 2 && r.o1 ? od[NB - 1].inv_m : od[0].inv_m;
-                    float iI = NOBJ == 2 && r.o1 ? od[NB - 1].iI : od[0].iI;
-                    obj_add(r.o1, ANISO ? r.wI[0] * -dl : r.rn[0] * (-dl * iI), r.dir[0] * (-dl * im));
+                for (int a = 0; a < 9; a++) dv[a] = fmaf(mj[a], dl, dv[a]);
+                if constexpr (NOBJ == 1) {
+                    // one object: fma straight into its velocity change
+                    dw[0] = ANISO ? fma3(r.wI[0], -dl, dw[0]) : fma3(r.rn[0], -dl * od[0].iI, dw[0]);
+                    dvl[0] = fma3(r.dir[0], -dl * od[0].inv_m, dvl[0]);
+                } else if constexpr (NOBJ == 2) {
+                    float im = r.o1 ? od[NB - 1].inv_m : od[0].inv_m;
+                    float iI = r.o1 ? od[NB - 1].iI : od[0].iI;
+                    obj_add(r.o1, r.rn[0] * (-dl * iI), r.dir[0] * (-dl * im));
                 }
                 res = fmaxf(res, fabsf(dl * res_scale(r.dinv[0])));
             }
@@ -1209,13 +1226,13 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     GroundContact &g = gc[b][c];
                     V3 r1 = mk(g.r.z, 0.0f, -g.r.x);  // r x (0,-1,0)
                     V3 r2 = mk(0.0f, g.r.z, -g.r.y);  // r x (1,0,0)
-                    float dla = g.rhs[1] - g.dinv[1] * (dot(r1, dw[b]) - dvl[b].y);
-                    float dlb = g.rhs[2] - g.dinv[2] * (dot(r2, dw[b]) + dvl[b].x);
+                    float dla = g.rhs[1] - g.dinv[1] * (r1.x * dw[b].x + r1.z * dw[b].z - dvl[b].y);
+                    float dlb = g.rhs[2] - g.dinv[2] * (r2.y * dw[b].y + r2.z * dw[b].z + dvl[b].x);
                     float sa = g.lam[1] + dla, sb = g.lam[2] + dlb;
                     float lim = gmu * fmaxf(g.lam[0], 0.0f);
                     float m2 = sa * sa + sb * sb;
                     // |f| > mu N: project onto the cone (lim * rsq(m2) <= 1 there)
-                    float s = m2 > lim * lim ? lim * rsqrtf(m2) : 1.0f;
+                    float s = cone_scale(m2, lim);
                     sa *= s;
                     sb *= s;
                     dla = sa - g.lam[1];
@@ -1251,7 +1268,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     float sa = p.lam[1] + dla, sb = p.lam[2] + dlb;
                     float lim = pmu * fmaxf(p.lam[0], 0.0f);
                     float m2 = sa * sa + sb * sb;
-                    float s = m2 > lim * lim ? lim * rsqrtf(m2) : 1.0f;
+                    float s = cone_scale(m2, lim);
                     sa *= s;
                     sb *= s;
                     dla = sa - p.lam[1];
@@ -1269,6 +1286,13 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         for (int c = 0; c < NR; c++)
             if (__builtin_amdgcn_ballot_w64(c < nr)) {
                 RobotContact &r = rc[c];
+                float mj1[9], mj2[9];
+#pragma unroll
+                for (int a = 0; a < 9; a++) {
+                    mj1[a] = L.at(c, 1, a);
+                    mj2[a] = L.at(c, 2, a);
+                }
+                __builtin_amdgcn_sched_barrier(0);
                 float ja = jrow_dot(r.J[1], dv), jb = jrow_dot(r.J[2], dv);
                 if (NOBJ > 0) {
                     V3 ow = obj_dw(r.o1), ov = obj_dv(r.o1);
@@ -1279,7 +1303,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 float sa = r.lam[1] + dla, sb = r.lam[2] + dlb;
                 float lim = r.mu * fmaxf(r.lam[0], 0.0f);
                 float m2 = sa * sa + sb * sb;
-                float s = m2 > lim * lim ? lim * rsqrtf(m2) : 1.0f;
+                float s = cone_scale(m2, lim);
                 sa *= s;
                 sb *= s;
                 dla = sa - r.lam[1];
@@ -1287,9 +1311,18 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 r.lam[1] = sa;
                 r.lam[2] = sb;
 #pragma unroll
-                for (int a = 0; a < 9; a++) dv[a] = fmaf(L.at(c, 2, a), dlb, fmaf(L.at(c, 1, a), dla, dv[a]));
-                if constexpr (NOBJ > 0) {
-                    float im = NOBJ == 2 && r.o1 ? od[NB - 1].inv_m : od[0].inv_m;
+                for (int a = 0; a < 9; a++) dv[a] = fmaf(mj2[a], dlb, fmaf(mj1[a], dla, dv[a]));
+                if constexpr (NOBJ == 1) {
+                    if constexpr (ANISO) {
+                        dw[0] = fma3(r.wI[2], -dlb, fma3(r.wI[1], -dla, dw[0]));
+                    } else {
+                        float aI = -dla * od[0].iI, bI = -dlb * od[0].iI;
+                        dw[0] = fma3(r.rn[2], bI, fma3(r.rn[1], aI, dw[0]));
+                    }
+                    float am = -dla * od[0].inv_m, bm = -dlb * od[0].inv_m;
+                    dvl[0] = fma3(r.dir[2], bm, fma3(r.dir[1], am, dvl[0]));
+                } else if constexpr (NOBJ == 2) {
+                    float im = r.o1 ? od[NB - 1].inv_m : od[0].inv_m;
                     V3 ddw;
                     if constexpr (ANISO) {
                         ddw = mk(fmaf(r.wI[2].x, -dlb, -dla * r.wI[1].x), fmaf(r.wI[2].y, -dlb, -dla * r.wI[1].y),

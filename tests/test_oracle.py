@@ -254,3 +254,30 @@ def test_pick_and_place_conditioning():
     pnp = _perturbed_step_spread("pick_and_place", "ee")
     assert push[:3].max() < 1e-5
     assert pnp[:3].max() > 10 * push[:3].max()
+
+
+@pytest.mark.parametrize("task", ["push", "stack"])
+def test_threaded_batch_step_matches_serial(task):
+    """po_step_batch over OpenMP threads (bench.py's cpu_baseline leg) gives the
+    serial loop's results bit for bit: envs share no mutable state."""
+    cfg = O.config(task)
+    n, na, od = 24, O.action_dim(cfg), O.obs_dim(cfg)
+    fp = lambda a: a.ctypes.data_as(O.C.POINTER(O.C.c_float))
+    u8 = lambda a: a.ctypes.data_as(O.C.POINTER(O.C.c_uint8))
+    acts = np.random.default_rng(5).uniform(-1, 1, size=(4, n, na)).astype(np.float32)
+    outs = []
+    for threads in (1, 4):
+        assert O.lib().po_set_threads(threads) >= 1
+        envs = (O.Env * n)()
+        for i in range(n):
+            O.lib().po_init_env(O.C.byref(cfg), O.C.byref(envs[i]))
+            O.lib().po_reset(O.C.byref(cfg), O.C.byref(envs[i]), 1, 100 + i, None, None, None)
+        obs = np.zeros((n, od), np.float32)
+        ag, dg = np.zeros((n, 6), np.float32), np.zeros((n, 6), np.float32)
+        rew, te, tr = np.zeros(n, np.float32), np.zeros(n, np.uint8), np.zeros(n, np.uint8)
+        for a in acts:
+            O.lib().po_step_batch(O.C.byref(cfg), envs, n, fp(a), fp(obs), fp(ag), fp(dg), fp(rew), u8(te), u8(tr),
+                                  1, None)
+        outs.append((obs.copy(), rew.copy()))
+    O.lib().po_set_threads(1)
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
