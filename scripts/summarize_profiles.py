@@ -128,6 +128,9 @@ def main():
         traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
         traffic[args.workload] = {"bytes_per_launch": round(kernels[step[0]]["hbm_bytes_per_launch"]),
                                   "source": f"profiles/{args.tag}_summary.json", "fetch_factor": factor}
+        sq = kernels[step[0]].get("sq_counters_per_launch", {})
+        if "SQ_INSTS_VALU" in sq:
+            traffic[args.workload]["valu_insts_per_launch"] = round(sq["SQ_INSTS_VALU"])
         json.dump(traffic, open(tpath, "w"), indent=1)
     for k, e in sorted(kernels.items(), key=lambda kv: -kv[1]["avg_ns_all"] * kv[1]["launches"])[:4]:
         print(k, {x: (round(v, 1) if isinstance(v, float) else v) for x, v in e.items()
