@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PS_ABI_VERSION 2
+#define PS_ABI_VERSION 3
 
 /* the six registered tasks (panda_gym/__init__.py:8-54) */
 enum {
@@ -44,6 +44,7 @@ enum {
 enum { PS_CONTROL_EE = 0, PS_CONTROL_JOINTS = 1 };
 enum { PS_REWARD_SPARSE = 0, PS_REWARD_DENSE = 1 };
 enum { PS_SHAPE_BOX = 0, PS_SHAPE_CYLINDER = 1 };
+#define PS_VISUAL_SPHERE 2 /* ps_visual.target_shape only: create_sphere ghost (reach.py:31-38) */
 enum { PS_OK = 0, PS_ERR_ARG = -1, PS_ERR_HIP = -2, PS_ERR_UNSUPPORTED = -3 };
 
 /* Scene/env configuration.  ps_default_config() fills the registered env
@@ -190,6 +191,49 @@ int ps_base_state(ps_ctx *ctx, const void *state, int object, float *pos, float 
  * rounded to f32) when both are f32.  reward and success may be NULL. */
 int ps_compute_reward(int task, int reward_type, const void *ag, int ag_is_double, const void *dg,
                       int dg_is_double, float *reward, uint8_t *success, int64_t n, void *stream);
+
+
+/* --- camera images (pybullet.py:69-264; §8(f) rank 4) --- */
+
+/* Visual description of the scene for ps_render: flat colours (r, g, b, a in
+ * [0, 1]) by role -- 0 plane, 1 table, 2 object 1, 3 object 2, 4 target 1,
+ * 5 target 2, 6 robot, 7 background -- and the ghost targets' shapes
+ * (PS_SHAPE_BOX, PS_SHAPE_CYLINDER, PS_VISUAL_SPHERE; -1 = none) with box half
+ * extents / cylinder (radius, radius, half height) / sphere (radius, ...). */
+typedef struct {
+    float rgba[8][4];
+    int32_t target_shape[2];
+    float target_half[2][3];
+} ps_visual;
+
+/* computeViewMatrixFromYawPitchRoll(target, distance, yaw, pitch, roll,
+ * upAxisIndex=2) and computeProjectionMatrixFOV(fov=60, aspect=width/height,
+ * near=0.1, far=100) as column-major float[16] (pybullet.py:69-107), and
+ * tran_pix_world = inv(P V) of the order='F' matrices, row-major double[16]
+ * (may be NULL).  Host arithmetic only: no context, no GPU. */
+int ps_camera(const float target[3], float distance, float yaw, float pitch, float roll, int width, int height,
+              float view[16], float proj[16], double tran_pix_world[16]);
+
+/* getCameraImage(width, height, view, proj) of every env (pybullet.py:186-192):
+ * depth [B, height, width] f32 (OpenGL window depth, 1 = nothing hit) and rgb
+ * [B, height, width, 3] u8, either may be NULL.  targets: device [B, 2, 7] f32
+ * ghost-target poses (position, quaternion x,y,z,w), NULL = no targets.  The
+ * arm is drawn as capsules between its joint frames plus the gripper spheres
+ * (the URDF meshes are not available); the rest of the scene is exact. */
+int ps_render(ps_ctx *ctx, const void *state, const float view[16], const float proj[16], int width, int height,
+              const ps_visual *vis, const float *targets, float *depth, uint8_t *rgb, void *stream);
+
+/* render()'s deprojection (pybullet.py:203-262) of depth [B, h, w]: per pixel
+ * the world point [B, h*w, 3] f64, valid [B, h*w] u8 (depth < 0.99 and
+ * 0 < z < 0.67 and -0.5 < x < 0.2) and pixels_2d [B, h*w, 2] f64; outputs may
+ * be NULL.  tran_pix_world: HOST row-major double[16]. */
+int ps_deproject_image(ps_ctx *ctx, const float *depth, const double tran_pix_world[16], int width, int height,
+                       double *points, uint8_t *valid, double *pixels_2d, void *stream);
+
+/* PyBullet.deproject(depth, pixels, tran_pix_world) (pybullet.py:109-146):
+ * n pixels (column, row) int32 per env [B, n, 2] -> points [B, n, 3] f64. */
+int ps_deproject_pixels(ps_ctx *ctx, const float *depth, const int32_t *pixels, int n,
+                        const double tran_pix_world[16], int width, int height, double *points, void *stream);
 
 #ifdef __cplusplus
 }

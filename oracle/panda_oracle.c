@@ -259,6 +259,29 @@ void po_link_state(const po_config *cfg, const po_env *env, int link, double pos
     }
 }
 
+/* World frames of all links (the rendering proxies' joint frames) and the
+ * world centres / radii of the gripper spheres (test infrastructure for the
+ * camera-image oracle, oracle/render_oracle.py). */
+void po_link_frames(const po_config *cfg, const po_env *env, double R[][9], double o[][3]) {
+    model_init();
+    okin k;
+    fk(cfg, env->q, &k);
+    memcpy(R, k.R, sizeof k.R);
+    memcpy(o, k.o, sizeof k.o);
+}
+
+void po_gripper_spheres(const po_config *cfg, const po_env *env, double c[][3], double r[]) {
+    model_init();
+    okin k;
+    fk(cfg, env->q, &k);
+    for (int s = 0; s < PM_NUM_SPHERES; s++) {
+        double w[3];
+        m3_vec(k.R[SPH[s].link], SPH[s].c, w);
+        for (int d = 0; d < 3; d++) c[s][d] = k.o[SPH[s].link][d] + w[d];
+        r[s] = SPH[s].r;
+    }
+}
+
 /* ------------------------------------------------------------- dynamics */
 static void mass_matrix(const okin *k, double M[81]) {
     memset(M, 0, sizeof(double) * 81);

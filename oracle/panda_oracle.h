@@ -78,6 +78,8 @@ void po_link_state(const po_config *cfg, const po_env *env, int link, double pos
 void po_inverse_kinematics(const po_config *cfg, const double q_start[9], int link, const double pos[3],
                            const double orn[4], double q_out[9]);
 void po_control_joints(po_env *env, int n, const int32_t *joints, const double *targets, const double *forces);
+void po_link_frames(const po_config *cfg, const po_env *env, double R[][9], double o[][3]);
+void po_gripper_spheres(const po_config *cfg, const po_env *env, double c[][3], double r[]);
 void po_substep(const po_config *cfg, po_env *env, po_stats *stats);
 void po_sim_step(const po_config *cfg, po_env *env, po_stats *stats);
 void po_euler_from_quaternion(const double q[4], double rpy[3]);

@@ -9,6 +9,7 @@
 
 #include "pandasim.h"
 #include "ps_physics.h"
+#include "ps_render.h"
 #include "ps_task.h"
 
 using namespace ps;
@@ -19,6 +20,7 @@ struct ps_ctx {
     ps_layout lay;
     int device;
     char err[256];
+    float *render_prims;  // [B][RENDER_PRIM_FLOATS] scratch of ps_render, allocated on first use
 };
 
 #ifdef PS_PROFILE_PHASES
@@ -696,6 +698,268 @@ __global__ __launch_bounds__(256) void k_compute_reward(int task, int reward_typ
     }
 }
 
+
+// ------------------------------------------------------------- rendering
+// Camera of a view/projection pair (column-major float[16], as getCameraImage
+// takes them): eye, the view axes (s, u, -f rows of the rotation) and the
+// projection terms a pixel ray and the depth buffer need.
+struct Cam {
+    V3 eye, s, u, f;
+    float p00, p11, p22, p23, nearv, farv;
+    float light[3];
+};
+
+Cam cam_of(const float view[16], const float proj[16]) {
+    Cam c;
+    // V = [R | t] (row r, col k = view[k*4 + r]); eye = -R^T t
+    c.s = mk(view[0], view[4], view[8]);
+    c.u = mk(view[1], view[5], view[9]);
+    c.f = mk(-view[2], -view[6], -view[10]);
+    V3 t = mk(view[12], view[13], view[14]);
+    c.eye = mk(-(c.s.x * t.x + c.u.x * t.y - c.f.x * t.z), -(c.s.y * t.x + c.u.y * t.y - c.f.y * t.z),
+               -(c.s.z * t.x + c.u.z * t.y - c.f.z * t.z));
+    c.p00 = proj[0];
+    c.p11 = proj[5];
+    c.p22 = proj[10];
+    c.p23 = proj[14];
+    // clip planes of the perspective matrix: z_ndc = -1 / +1
+    c.nearv = proj[14] / (proj[10] - 1.0f);
+    c.farv = proj[14] / (proj[10] + 1.0f);
+    // a fixed key light from above and behind the camera
+    V3 l = c.u * 0.6f - c.f * 0.3f + mk(0.0f, 0.0f, 0.7f);
+    float ln = 1.0f / sqrtf(dot(l, l));
+    c.light[0] = l.x * ln;
+    c.light[1] = l.y * ln;
+    c.light[2] = l.z * ln;
+    return c;
+}
+
+// Per-env primitives: the arm's capsules (joint frame to joint frame), the
+// gripper spheres, object and target poses.  One lane per env.
+__global__ __launch_bounds__(kBlock) void k_render_prep(KParams P, int n_objects, const float *targets, float *prims) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P.n) return;
+    const StateView &s = P.s;
+    float q[9], qd[9];
+    load_robot(s, i, q, qd);
+    Kin k;
+    fk(q, k);
+    float *o = prims + i * RENDER_PRIM_FLOATS;
+    const V3 b = P.sc.base;
+    auto put3 = [&](int at, V3 v) { o[at] = v.x; o[at + 1] = v.y; o[at + 2] = v.z; };
+    // link0 column, upper arm, elbow offsets, forearm, wrist, flange, hand bar
+    const V3 hand_a = k.f[8].o + mul(k.f[8].R, mk(0.0f, -0.09f, 0.03f));
+    const V3 hand_b = k.f[8].o + mul(k.f[8].R, mk(0.0f, 0.09f, 0.03f));
+    const V3 wrist = k.f[8].o + mul(k.f[8].R, mk(0.0f, 0.0f, 0.04f));  // flange -> palm (hand origin = flange)
+    const V3 A[RENDER_CAPSULES] = {mk(0, 0, 0), k.f[1].o, k.f[2].o, k.f[3].o, k.f[5].o, k.f[6].o, k.f[7].o, hand_a};
+    const V3 Bp[RENDER_CAPSULES] = {k.f[0].o, k.f[2].o, k.f[3].o, k.f[4].o, k.f[6].o, k.f[7].o, wrist, hand_b};
+    const float R[RENDER_CAPSULES] = {0.07f, 0.065f, 0.06f, 0.06f, 0.055f, 0.05f, 0.045f, 0.03f};
+#pragma unroll
+    for (int c = 0; c < RENDER_CAPSULES; c++) {
+        put3(RP_CAPS + c * 7, A[c] + b);
+        put3(RP_CAPS + c * 7 + 3, Bp[c] + b);
+        o[RP_CAPS + c * 7 + 6] = R[c];
+    }
+    static_for<0, PM_NUM_SPHERES>([&](auto SS) {
+        constexpr int S = decltype(SS)::value;
+        constexpr SphereDef d = sphere_def(S);
+        V3 c = k.f[d.link].o + mul(k.f[d.link].R, mk((float)d.c[0], (float)d.c[1], (float)d.c[2])) + b;
+        put3(RP_SPH + S * 4, c);
+        o[RP_SPH + S * 4 + 3] = (float)d.r;
+    });
+    for (int ob = 0; ob < 2; ob++) {
+        Body bd;
+        if (ob < n_objects) load_body(s, i, ob, bd);
+        else bd = Body{mk(0, 0, -100.0f), Q4{0, 0, 0, 1}, mk(0, 0, 0), mk(0, 0, 0)};
+        M3 Rm = quat_to_mat(bd.quat);
+        put3(RP_OBJ + ob * 12, bd.pos);
+        for (int e = 0; e < 9; e++) o[RP_OBJ + ob * 12 + 3 + e] = Rm.m[e];
+        V3 tp = mk(0, 0, -100.0f);
+        Q4 tq = Q4{0, 0, 0, 1};
+        if (targets) {
+            const float *t = targets + (i * 2 + ob) * 7;
+            tp = mk(t[0], t[1], t[2]);
+            tq = Q4{t[3], t[4], t[5], t[6]};
+        }
+        M3 Rt = quat_to_mat(tq);
+        put3(RP_TGT + ob * 12, tp);
+        for (int e = 0; e < 9; e++) o[RP_TGT + ob * 12 + 3 + e] = Rt.m[e];
+    }
+}
+
+struct RenderArgs {
+    Cam cam;
+    int width, height, n_objects, object_shape;
+    V3 object_half, table_c, table_h;
+    int has_table, has_plane;
+    ps_visual vis;
+};
+
+PS_D M3 m3_at(const float *p) {
+    M3 R;
+#pragma unroll
+    for (int e = 0; e < 9; e++) R.m[e] = p[e];
+    return R;
+}
+
+// getCameraImage (pybullet.py:186-192) by ray casting: one lane per pixel,
+// blockIdx.y = env.  Pixel (row r, col c) is sampled at its centre, as a
+// rasteriser does; depth is OpenGL window depth of the projection matrix.
+constexpr int kRenderBlock = 256;
+constexpr int kRenderPix = 4;  // pixels per lane (strided by the block)
+
+__global__ __launch_bounds__(kRenderBlock) void k_render(RenderArgs a, const float *prims, float *depth, uint8_t *rgb) {
+    __shared__ float pr[RENDER_PRIM_FLOATS];
+    const int64_t env = blockIdx.y;
+    for (int k = threadIdx.x; k < RENDER_PRIM_FLOATS; k += kRenderBlock) pr[k] = prims[env * RENDER_PRIM_FLOATS + k];
+    __syncthreads();
+    const Cam &cm = a.cam;
+    const int64_t npix = (int64_t)a.width * a.height;
+    const M3 I3 = M3{{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+    for (int pp = 0; pp < kRenderPix; pp++) {
+        int64_t pix = ((int64_t)blockIdx.x * kRenderPix + pp) * kRenderBlock + threadIdx.x;
+        if (pix >= npix) break;
+        int r = (int)(pix / a.width), c = (int)(pix - (int64_t)r * a.width);
+        float xn = -1.0f + (2.0f * c + 1.0f) / a.width, yn = 1.0f - (2.0f * r + 1.0f) / a.height;
+        // eye-space direction (xn / P00, yn / P11, -1): unit length along f, so t = -z_eye
+        V3 d = cm.s * (xn / cm.p00) + cm.u * (yn / cm.p11) + cm.f;
+        V3 o = cm.eye;
+        Hit h{cm.farv, mk(0, 0, 1)};
+        int role = VR_BACKGROUND;
+        const float tmin = cm.nearv;
+        if (a.has_plane && ray_box(o, d, mk(0, 0, (float)PM_PLANE_TOP - 0.01f), I3, mk(3.0f, 3.0f, 0.01f), tmin, h))
+            role = VR_PLANE;
+        if (a.has_table && ray_box(o, d, a.table_c, I3, a.table_h, tmin, h)) role = VR_TABLE;
+        for (int ob = 0; ob < a.n_objects; ob++) {
+            const float *q = pr + RP_OBJ + ob * 12;
+            V3 c0 = mk(q[0], q[1], q[2]);
+            M3 R = m3_at(q + 3);
+            bool hit = a.object_shape == PS_SHAPE_CYLINDER
+                           ? ray_cylinder(o, d, c0, R, a.object_half.x, a.object_half.z, tmin, h)
+                           : ray_box(o, d, c0, R, a.object_half, tmin, h);
+            if (hit) role = VR_OBJECT1 + ob;
+        }
+        for (int k = 0; k < RENDER_CAPSULES; k++) {
+            const float *q = pr + RP_CAPS + k * 7;
+            if (ray_capsule(o, d, mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), q[6], tmin, h)) role = VR_ROBOT;
+        }
+        for (int k = 0; k < PM_NUM_SPHERES; k++) {
+            const float *q = pr + RP_SPH + k * 4;
+            if (ray_sphere(o, d, mk(q[0], q[1], q[2]), q[3], tmin, h)) role = VR_ROBOT;
+        }
+        float dep = 1.0f;
+        const float *col = a.vis.rgba[role];
+        float cr = col[0], cg = col[1], cb = col[2];
+        if (role != VR_BACKGROUND) {
+            float ze = -h.t;
+            dep = 0.5f * ((cm.p22 * ze + cm.p23) / h.t) + 0.5f;
+            float nl = fabsf(h.n.x * cm.light[0] + h.n.y * cm.light[1] + h.n.z * cm.light[2]);
+            float sh = 0.35f + 0.65f * nl;
+            cr *= sh;
+            cg *= sh;
+            cb *= sh;
+        }
+        // ghost targets: alpha-blended over whatever is behind, no depth write
+        for (int g = 0; g < 2; g++) {
+            int shape = a.vis.target_shape[g];
+            if (shape < 0) continue;
+            const float *q = pr + RP_TGT + g * 12;
+            V3 c0 = mk(q[0], q[1], q[2]);
+            M3 R = m3_at(q + 3);
+            V3 hh = mk(a.vis.target_half[g][0], a.vis.target_half[g][1], a.vis.target_half[g][2]);
+            Hit gh{h.t, mk(0, 0, 1)};
+            bool hit = shape == PS_SHAPE_CYLINDER ? ray_cylinder(o, d, c0, R, hh.x, hh.z, tmin, gh)
+                       : shape == PS_VISUAL_SPHERE ? ray_sphere(o, d, c0, hh.x, tmin, gh)
+                                                   : ray_box(o, d, c0, R, hh, tmin, gh);
+            if (hit) {
+                const float *tc = a.vis.rgba[VR_TARGET1 + g];
+                float al = tc[3];
+                cr = al * tc[0] + (1.0f - al) * cr;
+                cg = al * tc[1] + (1.0f - al) * cg;
+                cb = al * tc[2] + (1.0f - al) * cb;
+            }
+        }
+        int64_t at = env * npix + pix;
+        if (depth) depth[at] = dep;
+        if (rgb) {
+            rgb[at * 3 + 0] = (uint8_t)fminf(fmaxf(cr * 255.0f + 0.5f, 0.0f), 255.0f);
+            rgb[at * 3 + 1] = (uint8_t)fminf(fmaxf(cg * 255.0f + 0.5f, 0.0f), 255.0f);
+            rgb[at * 3 + 2] = (uint8_t)fminf(fmaxf(cb * 255.0f + 0.5f, 0.0f), 255.0f);
+        }
+    }
+}
+
+struct Tran {
+    double m[16];  // row-major inv(P V)
+};
+
+// tran @ (x, y, z, 1) with the accumulation OpenBLAS's dgemm kernel uses for a
+// 4-deep product (one fused multiply-add per term, k ascending), then the
+// homogeneous divide (pybullet.py:140-143, 225-229)
+PS_D void pix_to_world(const Tran &T, double x, double y, double z, double out[3]) {
+    double w = fma(T.m[15], 1.0, fma(T.m[14], z, fma(T.m[13], y, T.m[12] * x)));
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        double v = fma(T.m[r * 4 + 3], 1.0, fma(T.m[r * 4 + 2], z, fma(T.m[r * 4 + 1], y, T.m[r * 4 + 0] * x)));
+        out[r] = v / w;
+    }
+}
+
+// render()'s post-processing of getCameraImage's depth (pybullet.py:203-262),
+// per env and pixel: NDC of np.mgrid (left/top pixel edges, the reference's
+// convention), valid = depth < 0.99 and the workspace box on the world point,
+// the world point and pixels_2d.
+__global__ __launch_bounds__(256) void k_deproject_image(int64_t n_env, int width, int height, Tran T,
+                                                         const float *depth, double *points, uint8_t *valid,
+                                                         double *pix2d) {
+#pragma clang fp contract(off)
+    int64_t npix = (int64_t)width * height;
+    int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_env * npix) return;
+    int64_t pix = g % npix;
+    int r = (int)(pix / width), c = (int)(pix - (int64_t)r * width);
+    // np.mgrid[-1:1:2/h, -1:1:2/w]: index * step + start; then y *= -1
+    double x = opaque(__dmul_rn((double)c, 2.0 / width)) + -1.0;
+    double y = -(opaque(__dmul_rn((double)r, 2.0 / height)) + -1.0);
+    double z = (double)depth[g];
+    double zn = opaque(__dmul_rn(2.0, z)) - 1.0;
+    double p[3];
+    pix_to_world(T, x, y, zn, p);
+    bool ok = z < 0.99 && p[2] > 0.0 && p[2] < 0.67 && p[0] > -0.5 && p[0] < 0.2;
+    if (valid) valid[g] = ok;
+    if (points) {
+        points[g * 3 + 0] = p[0];
+        points[g * 3 + 1] = p[1];
+        points[g * 3 + 2] = p[2];
+    }
+    if (pix2d) {
+        // (xy + 1) / 2, x *= w, y *= h, y = h - y
+        double px = opaque(x + 1.0) / 2.0, py = opaque(y + 1.0) / 2.0;
+        pix2d[g * 2 + 0] = px * (double)width;
+        pix2d[g * 2 + 1] = (double)height - opaque(py * (double)height);
+    }
+}
+
+// PyBullet.deproject(depth, pixels, tran_pix_world) (pybullet.py:109-146) for
+// n pixels (col, row) per env
+__global__ __launch_bounds__(256) void k_deproject_pixels(int64_t n_env, int n, int width, int height, Tran T,
+                                                          const float *depth, const int32_t *pixels, double *points) {
+#pragma clang fp contract(off)
+    int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= n_env * n) return;
+    int64_t env = g / n;
+    int pc = pixels[g * 2 + 0], prow = pixels[g * 2 + 1];
+    // x = px / w * 2 - 1 ; y = (h - py) / h * 2 - 1 ; z = 2 depth[py, px] - 1
+    double x = opaque(opaque((double)pc * (1.0 / width)) * 2.0) - 1.0;
+    double y = opaque(opaque((double)(height - prow) * (1.0 / height)) * 2.0) - 1.0;
+    double z = opaque(2.0 * (double)depth[env * (int64_t)width * height + (int64_t)prow * width + pc]) - 1.0;
+    double p[3];
+    pix_to_world(T, x, y, z, p);
+    points[g * 3 + 0] = p[0];
+    points[g * 3 + 1] = p[1];
+    points[g * 3 + 2] = p[2];
+}
+
 // ----------------------------------------------------------- host helpers
 int fail(ps_ctx *c, int code, const char *msg) {
     if (c) snprintf(c->err, sizeof c->err, "%s", msg);
@@ -810,7 +1074,10 @@ int ps_create(const ps_config *cfg, int64_t num_envs, int device, ps_ctx **out) 
     return PS_OK;
 }
 
-void ps_destroy(ps_ctx *ctx) { delete ctx; }
+void ps_destroy(ps_ctx *ctx) {
+    if (ctx && ctx->render_prims) (void)hipFree(ctx->render_prims);
+    delete ctx;
+}
 
 const char *ps_last_error(const ps_ctx *ctx) { return ctx ? ctx->err : "null context"; }
 
@@ -979,6 +1246,87 @@ int ps_compute_reward(int task, int reward_type, const void *ag, int ag_is_doubl
     hipLaunchKernelGGL(k_compute_reward, grid_of(n, 256), dim3(256), 0, (hipStream_t)stream, task, reward_type, ag,
                        ag_is_double, dg, dg_is_double, reward, success, n);
     return hipGetLastError() == hipSuccess ? PS_OK : PS_ERR_HIP;
+}
+
+
+int ps_camera(const float target[3], float distance, float yaw, float pitch, float roll, int width, int height,
+              float view[16], float proj[16], double tran_pix_world[16]) {
+    if (!target || !view || !proj || width <= 0 || height <= 0) return PS_ERR_ARG;
+    ps_camera_math::view_from_yaw_pitch_roll(target, distance, yaw, pitch, roll, view);
+    ps_camera_math::projection_fov(60.0, (double)width / height, 0.1, 100.0, proj);
+    if (tran_pix_world) {
+        // np.linalg.inv(P @ V) of the reshape(order='F') matrices, in double
+        double P[16], V[16], PV[16];
+        for (int r = 0; r < 4; r++)
+            for (int c = 0; c < 4; c++) {
+                P[r * 4 + c] = proj[c * 4 + r];
+                V[r * 4 + c] = view[c * 4 + r];
+            }
+        for (int r = 0; r < 4; r++)
+            for (int c = 0; c < 4; c++) {
+                double acc = 0.0;
+                for (int k = 0; k < 4; k++) acc += P[r * 4 + k] * V[k * 4 + c];
+                PV[r * 4 + c] = acc;
+            }
+        if (!ps_camera_math::invert4(PV, tran_pix_world)) return PS_ERR_ARG;
+    }
+    return PS_OK;
+}
+
+int ps_render(ps_ctx *c, const void *state, const float view[16], const float proj[16], int width, int height,
+              const ps_visual *vis, const float *targets, float *depth, uint8_t *rgb, void *stream) {
+    if (!c || !state || !view || !proj || !vis || width <= 0 || height <= 0) return fail(c, PS_ERR_ARG, "null argument");
+    if (!c->render_prims) {
+        if (hipMalloc((void **)&c->render_prims, sizeof(float) * RENDER_PRIM_FLOATS * c->num_envs) != hipSuccess) {
+            c->render_prims = nullptr;
+            return fail(c, PS_ERR_HIP, "hipMalloc of the render scratch failed");
+        }
+    }
+    KParams P = params_of(c, (void *)state);
+    hipStream_t st = (hipStream_t)stream;
+    hipLaunchKernelGGL(k_render_prep, grid_of(P.n, kBlock), dim3(kBlock), 0, st, P, c->cfg.n_objects, targets,
+                       c->render_prims);
+    RenderArgs a;
+    a.cam = cam_of(view, proj);
+    a.width = width;
+    a.height = height;
+    a.n_objects = c->cfg.n_objects;
+    a.object_shape = c->cfg.object_shape;
+    a.object_half = mk(c->cfg.object_half[0], c->cfg.object_half[1], c->cfg.object_half[2]);
+    // create_table: box of half extents (length, width, height) / 2 at (x_offset, 0, -height / 2)
+    a.table_c = mk(c->cfg.table_cx, 0.0f, (float)PM_TABLE_TOP - 0.2f);
+    a.table_h = mk(c->cfg.table_hx, c->cfg.table_hy, 0.2f);
+    a.has_table = c->cfg.has_table;
+    a.has_plane = c->cfg.has_plane;
+    a.vis = *vis;
+    int64_t npix = (int64_t)width * height;
+    dim3 g((unsigned)((npix + kRenderBlock * kRenderPix - 1) / (kRenderBlock * kRenderPix)), (unsigned)c->num_envs);
+    hipLaunchKernelGGL(k_render, g, dim3(kRenderBlock), 0, st, a, c->render_prims, depth, rgb);
+    return check_launch(c);
+}
+
+int ps_deproject_image(ps_ctx *c, const float *depth, const double tran_pix_world[16], int width, int height,
+                       double *points, uint8_t *valid, double *pixels_2d, void *stream) {
+    if (!c || !depth || !tran_pix_world || width <= 0 || height <= 0) return fail(c, PS_ERR_ARG, "null argument");
+    Tran T;
+    memcpy(T.m, tran_pix_world, sizeof T.m);
+    int64_t n = c->num_envs * (int64_t)width * height;
+    hipLaunchKernelGGL(k_deproject_image, grid_of(n, 256), dim3(256), 0, (hipStream_t)stream, c->num_envs, width,
+                       height, T, depth, points, valid, pixels_2d);
+    return check_launch(c);
+}
+
+int ps_deproject_pixels(ps_ctx *c, const float *depth, const int32_t *pixels, int n, const double tran_pix_world[16],
+                        int width, int height, double *points, void *stream) {
+    if (!c || !depth || !pixels || !points || !tran_pix_world || n < 0 || width <= 0 || height <= 0)
+        return fail(c, PS_ERR_ARG, "null argument");
+    if (n == 0) return PS_OK;
+    Tran T;
+    memcpy(T.m, tran_pix_world, sizeof T.m);
+    int64_t tot = c->num_envs * (int64_t)n;
+    hipLaunchKernelGGL(k_deproject_pixels, grid_of(tot, 256), dim3(256), 0, (hipStream_t)stream, c->num_envs, n,
+                       width, height, T, depth, pixels, points);
+    return check_launch(c);
 }
 
 }  // extern "C"

@@ -37,6 +37,15 @@ class Config(C.Structure):
     ]
 
 
+class Visual(C.Structure):
+    """ps_visual (include/pandasim.h): colours by role and ghost-target shapes."""
+    _fields_ = [("rgba", (C.c_float * 4) * 8), ("target_shape", C.c_int32 * 2), ("target_half", (C.c_float * 3) * 2)]
+
+
+VISUAL_SPHERE = 2
+ROLES = ("plane", "table", "object1", "object2", "target1", "target2", "robot", "background")
+
+
 class Layout(C.Structure):
     _fields_ = [
         ("num_envs", C.c_int64), ("stride", C.c_int64), ("float_offset", C.c_int64), ("goal_offset", C.c_int64),
@@ -56,7 +65,8 @@ def exported_symbols():
         "ps_abi_version", "ps_default_config", "ps_state_layout", "ps_create", "ps_destroy", "ps_last_error",
         "ps_obs_dim", "ps_action_dim", "ps_goal_dim", "ps_max_episode_steps", "ps_init_state", "ps_reset",
         "ps_step", "ps_sim_step", "ps_link_state", "ps_inverse_kinematics", "ps_compute_reward", "ps_rng_seed",
-        "ps_rng_uniform", "ps_rng_rotation", "ps_base_state",
+        "ps_rng_uniform", "ps_rng_rotation", "ps_base_state", "ps_camera", "ps_render", "ps_deproject_image",
+        "ps_deproject_pixels",
     ]
 
 
@@ -92,6 +102,11 @@ def lib():
     L.ps_rng_uniform.argtypes = [V, V, V, I, P(C.c_double), P(C.c_double), V, V]
     L.ps_rng_rotation.argtypes = [V, V, V, V, V]
     L.ps_base_state.argtypes = [V, V, I, V, V, V, V, V, V]
+    F, D = P(C.c_float), P(C.c_double)
+    L.ps_camera.argtypes = [F, C.c_float, C.c_float, C.c_float, C.c_float, I, I, F, F, D]
+    L.ps_render.argtypes = [V, V, F, F, I, I, P(Visual), V, V, V, V]
+    L.ps_deproject_image.argtypes = [V, V, D, I, I, V, V, V, V]
+    L.ps_deproject_pixels.argtypes = [V, V, V, I, D, I, I, V, V]
     for name in exported_symbols():
         getattr(L, name).restype = getattr(L, name).restype if name in ("ps_destroy", "ps_last_error") else I
     _lib = L

@@ -63,6 +63,9 @@ class PandaSim:
             self._objects[name] = k
         self._ghost_pos: Dict[str, torch.Tensor] = {}
         self._ghost_orn: Dict[str, torch.Tensor] = {}
+        # visual-only properties of created bodies (rgba, ghost shape): rendering
+        self._rgba: Dict[str, np.ndarray] = {}
+        self._ghost_shape: Dict[str, tuple] = {}
         self.layout = L.layout(self.num_envs)
         self.state = torch.zeros(self.layout.total_bytes, dtype=torch.uint8, device=self.device)
         self._bind_views()
@@ -152,7 +155,7 @@ class PandaSim:
     # Reach/Push/PickAndPlace scenes and raise NotImplementedError otherwise.
     @contextlib.contextmanager
     def no_rendering(self):
-        """pybullet.py:502-507 (rendering is not part of this path)."""
+        """pybullet.py:502-507: GUI rendering toggle; images come from render()."""
         yield
 
     def place_visualizer(self, target_position=None, distance=None, yaw=None, pitch=None) -> None:
@@ -217,6 +220,7 @@ class PandaSim:
     def create_box(self, body_name: str, half_extents, mass: float, position, rgba_color=None, specular_color=None,
                    ghost: bool = False, lateral_friction=None, spinning_friction=None, texture=None) -> None:
         """pybullet.py:516-582: a dynamic cube (Push/PickAndPlace/Flip; two for Stack) or a ghost marker."""
+        self._note_visual(body_name, rgba_color, L.SHAPE_BOX, [float(x) for x in half_extents], ghost)
         if ghost:
             self._add_ghost(body_name, position)
             return
@@ -228,6 +232,7 @@ class PandaSim:
                         specular_color=None, ghost: bool = False, lateral_friction=None,
                         spinning_friction=None) -> None:
         """pybullet.py:584-623: the upright cylinder of Slide (axis z), or a ghost marker."""
+        self._note_visual(body_name, rgba_color, L.SHAPE_CYLINDER, [radius, radius, height / 2], ghost)
         if ghost:
             self._add_ghost(body_name, position)
             return
@@ -238,6 +243,7 @@ class PandaSim:
     def create_sphere(self, body_name: str, radius: float, mass: float, position, rgba_color=None,
                       specular_color=None, ghost: bool = False) -> None:
         """pybullet.py:665-693: ghost target markers only."""
+        self._note_visual(body_name, rgba_color, L.VISUAL_SPHERE, [radius, radius, radius], ghost)
         if not ghost:
             raise NotImplementedError("create_sphere: only ghost spheres (targets) are supported")
         self._add_ghost(body_name, position)
@@ -252,6 +258,12 @@ class PandaSim:
         if not (self._bodies.get(body) == "robot" and int(link) in (9, 10) and spinning_friction == 0.001):
             raise NotImplementedError("set_spinning_friction: only the Panda fingers' 0.001 is compiled in")
 
+    def _note_visual(self, body_name, rgba_color, shape, half, ghost) -> None:
+        rgba = np.zeros(4) if rgba_color is None else np.asarray(rgba_color, np.float64)  # pybullet.py:536
+        self._rgba[body_name] = rgba
+        if ghost:
+            self._ghost_shape[body_name] = (shape, [float(h) for h in half])
+
     def _add_ghost(self, body_name: str, position) -> None:
         self._bodies[body_name] = "ghost"
         self._ghost_pos[body_name] = torch.zeros(self.num_envs, 3, dtype=torch.float64, device=self.device)
@@ -263,6 +275,169 @@ class PandaSim:
         if body not in self._bodies:
             raise KeyError(f"unknown body {body!r}")
         return self._bodies[body]
+
+    # ----------------------------------------------------- camera images
+    # pybullet.py:69-264 (§8(f) rank 4).  Batched: one image per env.
+    def get_cam2world_transforms(self, width: int = 480, height: int = 480, target_position=np.zeros(3),
+                                 distance: float = 1.4, yaw: float = 45, pitch: float = -30, roll: float = 0):
+        """pybullet.py:69-107: (view_matrix, proj_matrix) as pybullet's 16-float
+        tuples and tran_pix_world = inv(P @ V) (4, 4) float64."""
+        target_position = np.zeros(3) if target_position is None else target_position
+        t = (C.c_float * 3)(*[float(x) for x in target_position])
+        view, proj, tran = (C.c_float * 16)(), (C.c_float * 16)(), (C.c_double * 16)()
+        L.check(self._lib.ps_camera(t, float(distance), float(yaw), float(pitch), float(roll), int(width),
+                                    int(height), view, proj, tran), what="ps_camera")
+        return tuple(view[:]), tuple(proj[:]), np.array(tran[:], np.float64).reshape(4, 4)
+
+    def _visual(self) -> L.Visual:
+        """Colours by role and ghost-target shapes: from the create_* calls of
+        the plugin path, else the registered task's _create_scene (tasks/*.py)."""
+        v = L.Visual()
+        cols = {"plane": (0.15, 0.15, 0.15, 1.0), "table": (0.95, 0.95, 0.95, 1.0), "robot": (0.9, 0.9, 0.92, 1.0),
+                "background": (0.78, 0.85, 0.92, 1.0), "object1": (0.1, 0.9, 0.1, 1.0),
+                "object2": (0.1, 0.9, 0.1, 1.0), "target1": (0.1, 0.9, 0.1, 0.3), "target2": (0.1, 0.9, 0.1, 0.3)}
+        task = self.cfg.task
+        half = [float(self.cfg.object_half[k]) for k in range(3)]
+        shapes = [(L.SHAPE_BOX, half), (-1, [0.0] * 3)]
+        if task == TASKS["reach"]:
+            shapes[0] = (L.VISUAL_SPHERE, [0.02] * 3)  # reach.py:31-38
+        elif task == TASKS["slide"]:
+            shapes[0] = (L.SHAPE_CYLINDER, half)  # slide.py:43-51
+        elif task == TASKS["stack"]:  # stack.py:33-61: blue object1/target1, green object2/target2
+            cols.update(object1=(0.1, 0.1, 0.9, 1.0), target1=(0.1, 0.1, 0.9, 0.3))
+            shapes[1] = (L.SHAPE_BOX, half)
+        elif task == TASKS["flip"]:  # flip.py:33-47 (textured cube drawn in its mean colour)
+            cols.update(object1=(0.55, 0.55, 0.55, 1.0), target1=(1.0, 1.0, 1.0, 0.5))
+        objs = sorted(self._objects.items(), key=lambda kv: kv[1])
+        for name, k in objs:
+            if name in self._rgba:
+                cols[f"object{k + 1}"] = tuple(self._rgba[name])
+        ghosts = list(self._ghost_shape.items())
+        if ghosts:
+            shapes = [(-1, [0.0] * 3), (-1, [0.0] * 3)]
+            for g, (name, (shape, h)) in enumerate(ghosts[:2]):
+                shapes[g] = (shape, h)
+                cols[f"target{g + 1}"] = tuple(self._rgba[name])
+        for r, role in enumerate(L.ROLES):
+            for k in range(4):
+                v.rgba[r][k] = float(cols[role][k])
+        for g in range(2):
+            v.target_shape[g] = int(shapes[g][0])
+            for k in range(3):
+                v.target_half[g][k] = float(shapes[g][1][k])
+        return v
+
+    def _target_poses(self) -> torch.Tensor:
+        """[B, 2, 7] f32 ghost-target poses: the plugin path's set_base_pose
+        calls, else the fused path's goals as each task's reset places them
+        (reach.py:49, push.py:72, stack.py:97-98, flip.py:66)."""
+        B = self.num_envs
+        out = torch.zeros(B, 2, 7, dtype=torch.float32, device=self.device)
+        out[:, :, 6] = 1.0
+        out[:, :, 2] = -100.0
+        names = list(self._ghost_shape)[:2]
+        if names:
+            for g, n in enumerate(names):
+                out[:, g, :3] = self._ghost_pos[n].float()
+                out[:, g, 3:] = self._ghost_orn[n].float()
+            return out
+        goals = self.goals().float()
+        if self.cfg.task == TASKS["flip"]:
+            out[:, 0, :3] = torch.tensor([0.0, 0.0, 3 * 0.04 / 2], device=self.device)
+            out[:, 0, 3:] = goals[:, :4]
+        else:
+            out[:, 0, :3] = goals[:, :3]
+            if self.cfg.task == TASKS["stack"]:
+                out[:, 1, :3] = goals[:, 3:6]
+        return out
+
+    @staticmethod
+    def _check_image_size(width: int, height: int) -> None:
+        # render() builds its NDC grid with np.mgrid[-1:1:2/n], whose length is
+        # ceil(2 / (2/n)): for some n that is n + 1 and the reference's
+        # np.stack of the grid with the depth buffer raises
+        for n in (width, height):
+            if int(math.ceil(2.0 / (2.0 / n))) != n:
+                raise ValueError(f"render: np.mgrid[-1:1:2/{n}] has {int(math.ceil(2.0 / (2.0 / n)))} entries, not "
+                                 f"{n}; the reference's deprojection cannot stack it with a {n}-pixel axis")
+
+    def get_camera_image(self, width: int, height: int, view_matrix, proj_matrix, rgb: bool = True):
+        """getCameraImage (pybullet.py:186-192) of every env: depth [B, h, w]
+        f32 (OpenGL window depth) and rgb [B, h, w, 3] u8 (RGB order)."""
+        B = self.num_envs
+        depth = torch.empty(B, height, width, dtype=torch.float32, device=self.device)
+        img = torch.empty(B, height, width, 3, dtype=torch.uint8, device=self.device) if rgb else None
+        view = (C.c_float * 16)(*[float(x) for x in view_matrix])
+        proj = (C.c_float * 16)(*[float(x) for x in proj_matrix])
+        vis = self._visual()
+        targets = self._target_poses().contiguous()
+        self._call("ps_render", self._ctx, _ptr(self.state), view, proj, int(width), int(height), C.byref(vis),
+                   _ptr(targets), _ptr(depth), _ptr(img), self._stream())
+        return depth, img
+
+    def render(self, width: int = 480, height: int = 480, target_position=np.zeros(3), distance: float = 1.4,
+               yaw: float = 45, pitch: float = -30, roll: float = 0, waypoints=None, env: Optional[int] = None):
+        """PyBullet.render (pybullet.py:149-264) for every env.
+
+        env=None: a dict of batched tensors -- rgb [B, h, w, 3] u8 (channels
+        swapped as the reference's cv2.cvtColor(BGR2RGB) of pybullet's RGBA
+        leaves them), depth [B, h, w] f32, points [B, h*w, 3] f64, valid
+        [B, h*w] bool (the reference keeps points[valid[b]] in pixel order),
+        colors [B, h*w, 3] u8, pixels_2d [B, h*w, 2] f64, waypoints_proj.
+        env=i: the reference's tuple (rgb, depth, points, colors, pixels_2d,
+        waypoints_proj) of env i as numpy arrays."""
+        self._check_image_size(width, height)
+        view, proj, tran = self.get_cam2world_transforms(width, height, target_position, distance, yaw, pitch, roll)
+        depth, img = self.get_camera_image(width, height, view, proj)
+        B, n = self.num_envs, width * height
+        points = torch.empty(B, n, 3, dtype=torch.float64, device=self.device)
+        valid = torch.empty(B, n, dtype=torch.uint8, device=self.device)
+        pix2d = torch.empty(B, n, 2, dtype=torch.float64, device=self.device)
+        T = (C.c_double * 16)(*tran.reshape(-1).tolist())
+        self._call("ps_deproject_image", self._ctx, _ptr(depth), T, int(width), int(height), _ptr(points),
+                   _ptr(valid), _ptr(pix2d), self._stream())
+        waypoints_proj = []
+        if waypoints is not None:
+            PV = np.matmul(np.asarray(proj).reshape([4, 4], order="F"), np.asarray(view).reshape([4, 4], order="F"))
+            for point in waypoints:
+                x, y, z, w = np.matmul(PV, np.array([point[0], point[1], point[2], 1]))
+                x, y = (x / w + 1) / 2 * width, (y / w + 1) / 2 * height
+                waypoints_proj.append([int(x), int(height - y)])
+        out = {"rgb": img.flip(-1), "depth": depth, "points": points, "valid": valid.bool(),
+               "colors": img.reshape(B, n, 3), "pixels_2d": pix2d, "waypoints_proj": waypoints_proj}
+        if env is None:
+            return out
+        keep = out["valid"][env].cpu().numpy()
+        return (out["rgb"][env].cpu().numpy(), out["depth"][env].double().cpu().numpy(),
+                out["points"][env].cpu().numpy()[keep], out["colors"][env].cpu().numpy()[keep],
+                out["pixels_2d"][env].cpu().numpy()[keep], waypoints_proj)
+
+    def deproject(self, depth, pixels, tran_pix_world, width: int = 480, height: int = 480) -> torch.Tensor:
+        """PyBullet.deproject (pybullet.py:109-146) per env: depth [B, h, w]
+        (or one [h, w] image for every env), pixels [n, 2] or [B, n, 2]
+        (column, row) -> world points [B, n, 3] float64."""
+        B = self.num_envs
+        depth = torch.as_tensor(depth, device=self.device).to(torch.float32)
+        if depth.dim() == 2:
+            depth = depth.unsqueeze(0).expand(B, -1, -1)
+        depth = depth.contiguous()
+        pixels = torch.as_tensor(np.asarray(pixels) if not torch.is_tensor(pixels) else pixels,
+                                 device=self.device).to(torch.int32)
+        if pixels.dim() == 2:
+            pixels = pixels.unsqueeze(0).expand(B, -1, -1)
+        pixels = pixels.contiguous()
+        if depth.shape != (B, height, width) or pixels.shape[0] != B or pixels.shape[2] != 2:
+            raise ValueError(f"deproject: depth {tuple(depth.shape)} / pixels {tuple(pixels.shape)} do not match "
+                             f"{B} envs of {height}x{width}")
+        if pixels.numel() and (int(pixels[..., 0].min()) < 0 or int(pixels[..., 0].max()) >= width
+                               or int(pixels[..., 1].min()) < 0 or int(pixels[..., 1].max()) >= height):
+            raise IndexError("deproject: pixel outside the image")  # numpy's depth[rows, cols] raises too
+        n = pixels.shape[1]
+        points = torch.empty(B, n, 3, dtype=torch.float64, device=self.device)
+        T = (C.c_double * 16)(*np.asarray(tran_pix_world, np.float64).reshape(-1).tolist())
+        self._call("ps_deproject_pixels", self._ctx, _ptr(depth), _ptr(pixels), int(n), T, int(width), int(height),
+                   _ptr(points), self._stream())
+        return points
 
     # ------------------------------------------------------- per-env RNGs
     def seed(self, seeds, mask=None) -> None:

@@ -18,3 +18,10 @@ def golden():
     import numpy as np
 
     return dict(np.load(os.path.join(ROOT, "tests", "golden", "task_layer.npz")))
+
+
+@pytest.fixture(scope="session")
+def render_golden():
+    import numpy as np
+
+    return dict(np.load(os.path.join(ROOT, "tests", "golden", "render.npz")))
