@@ -949,9 +949,10 @@ __global__ __launch_bounds__(256) void k_deproject_pixels(int64_t n_env, int n, 
     if (g >= n_env * n) return;
     int64_t env = g / n;
     int pc = pixels[g * 2 + 0], prow = pixels[g * 2 + 1];
-    // x = px / w * 2 - 1 ; y = (h - py) / h * 2 - 1 ; z = 2 depth[py, px] - 1
-    double x = opaque(opaque((double)pc * (1.0 / width)) * 2.0) - 1.0;
-    double y = opaque(opaque((double)(height - prow) * (1.0 / height)) * 2.0) - 1.0;
+    // x = px * 1 / w (integer numerator, true division), x *= 2, x -= 1; the same for
+    // (h - py); z = 2 depth[py, px] - 1
+    double x = opaque(opaque((double)pc / (double)width) * 2.0) - 1.0;
+    double y = opaque(opaque((double)(height - prow) / (double)height) * 2.0) - 1.0;
     double z = opaque(2.0 * (double)depth[env * (int64_t)width * height + (int64_t)prow * width + pc]) - 1.0;
     double p[3];
     pix_to_world(T, x, y, z, p);
