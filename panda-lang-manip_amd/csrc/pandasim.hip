@@ -909,35 +909,45 @@ PS_D void pix_to_world(const Tran &T, double x, double y, double z, double out[3
 // per env and pixel: NDC of np.mgrid (left/top pixel edges, the reference's
 // convention), valid = depth < 0.99 and the workspace box on the world point,
 // the world point and pixels_2d.
-__global__ __launch_bounds__(256) void k_deproject_image(int64_t n_env, int width, int height, Tran T,
-                                                         const float *depth, double *points, uint8_t *valid,
-                                                         double *pix2d) {
+constexpr int kDeprojBlock = 256;
+
+__global__ __launch_bounds__(kDeprojBlock) void k_deproject_image(int64_t n_env, int width, int height, Tran T,
+                                                                  const float *depth, double *points,
+                                                                  uint8_t *valid, double *pix2d) {
 #pragma clang fp contract(off)
-    int64_t npix = (int64_t)width * height;
-    int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= n_env * npix) return;
-    int64_t pix = g % npix;
-    int r = (int)(pix / width), c = (int)(pix - (int64_t)r * width);
-    // np.mgrid[-1:1:2/h, -1:1:2/w]: index * step + start; then y *= -1
-    double x = opaque(__dmul_rn((double)c, 2.0 / width)) + -1.0;
-    double y = -(opaque(__dmul_rn((double)r, 2.0 / height)) + -1.0);
-    double z = (double)depth[g];
-    double zn = opaque(__dmul_rn(2.0, z)) - 1.0;
-    double p[3];
-    pix_to_world(T, x, y, zn, p);
-    bool ok = z < 0.99 && p[2] > 0.0 && p[2] < 0.67 && p[0] > -0.5 && p[0] < 0.2;
-    if (valid) valid[g] = ok;
-    if (points) {
-        points[g * 3 + 0] = p[0];
-        points[g * 3 + 1] = p[1];
-        points[g * 3 + 2] = p[2];
-    }
-    if (pix2d) {
+    // the block's points / pixels_2d are staged in LDS and leave as
+    // lane-contiguous 8-byte stores (a wave writes 512 contiguous bytes per
+    // instruction) instead of 24- and 16-byte strided ones
+    __shared__ double sp[kDeprojBlock * 3];
+    __shared__ double sx[kDeprojBlock * 2];
+    const int64_t npix = (int64_t)width * height, total = n_env * npix;
+    const int64_t g0 = (int64_t)blockIdx.x * kDeprojBlock, g = g0 + threadIdx.x;
+    if (g < total) {
+        int64_t pix = g % npix;
+        int r = (int)(pix / width), c = (int)(pix - (int64_t)r * width);
+        // np.mgrid[-1:1:2/h, -1:1:2/w]: index * step + start; then y *= -1
+        double x = opaque(__dmul_rn((double)c, 2.0 / width)) + -1.0;
+        double y = -(opaque(__dmul_rn((double)r, 2.0 / height)) + -1.0);
+        double z = (double)depth[g];
+        double zn = opaque(__dmul_rn(2.0, z)) - 1.0;
+        double p[3];
+        pix_to_world(T, x, y, zn, p);
+        bool ok = z < 0.99 && p[2] > 0.0 && p[2] < 0.67 && p[0] > -0.5 && p[0] < 0.2;
+        if (valid) valid[g] = ok;
+        sp[threadIdx.x * 3 + 0] = p[0];
+        sp[threadIdx.x * 3 + 1] = p[1];
+        sp[threadIdx.x * 3 + 2] = p[2];
         // (xy + 1) / 2, x *= w, y *= h, y = h - y
         double px = opaque(x + 1.0) / 2.0, py = opaque(y + 1.0) / 2.0;
-        pix2d[g * 2 + 0] = px * (double)width;
-        pix2d[g * 2 + 1] = (double)height - opaque(py * (double)height);
+        sx[threadIdx.x * 2 + 0] = px * (double)width;
+        sx[threadIdx.x * 2 + 1] = (double)height - opaque(py * (double)height);
     }
+    __syncthreads();
+    const int64_t n_here = total - g0 < kDeprojBlock ? total - g0 : kDeprojBlock;
+    if (points)
+        for (int k = threadIdx.x; k < n_here * 3; k += kDeprojBlock) points[g0 * 3 + k] = sp[k];
+    if (pix2d)
+        for (int k = threadIdx.x; k < n_here * 2; k += kDeprojBlock) pix2d[g0 * 2 + k] = sx[k];
 }
 
 // PyBullet.deproject(depth, pixels, tran_pix_world) (pybullet.py:109-146) for
@@ -1312,8 +1322,8 @@ int ps_deproject_image(ps_ctx *c, const float *depth, const double tran_pix_worl
     Tran T;
     memcpy(T.m, tran_pix_world, sizeof T.m);
     int64_t n = c->num_envs * (int64_t)width * height;
-    hipLaunchKernelGGL(k_deproject_image, grid_of(n, 256), dim3(256), 0, (hipStream_t)stream, c->num_envs, width,
-                       height, T, depth, points, valid, pixels_2d);
+    hipLaunchKernelGGL(k_deproject_image, grid_of(n, kDeprojBlock), dim3(kDeprojBlock), 0, (hipStream_t)stream,
+                       c->num_envs, width, height, T, depth, points, valid, pixels_2d);
     return check_launch(c);
 }
 
