@@ -767,6 +767,27 @@ __global__ __launch_bounds__(kBlock) void k_render_prep(KParams P, int n_objects
         put3(RP_SPH + S * 4, c);
         o[RP_SPH + S * 4 + 3] = (float)d.r;
     });
+    {
+        // bounding sphere of the arm's primitives: k_render skips them for rays that miss it
+        V3 lo = mk(3e38f, 3e38f, 3e38f), hi = mk(-3e38f, -3e38f, -3e38f);
+        auto grow = [&](V3 p) {
+            lo = mk(fminf(lo.x, p.x), fminf(lo.y, p.y), fminf(lo.z, p.z));
+            hi = mk(fmaxf(hi.x, p.x), fmaxf(hi.y, p.y), fmaxf(hi.z, p.z));
+        };
+        float rmax = 0.0f;
+        for (int c = 0; c < RENDER_CAPSULES; c++) {
+            grow(mk(o[RP_CAPS + c * 7], o[RP_CAPS + c * 7 + 1], o[RP_CAPS + c * 7 + 2]));
+            grow(mk(o[RP_CAPS + c * 7 + 3], o[RP_CAPS + c * 7 + 4], o[RP_CAPS + c * 7 + 5]));
+            rmax = fmaxf(rmax, o[RP_CAPS + c * 7 + 6]);
+        }
+        for (int c = 0; c < PM_NUM_SPHERES; c++) {
+            grow(mk(o[RP_SPH + c * 4], o[RP_SPH + c * 4 + 1], o[RP_SPH + c * 4 + 2]));
+            rmax = fmaxf(rmax, o[RP_SPH + c * 4 + 3]);
+        }
+        V3 ctr = (lo + hi) * 0.5f, half = (hi - lo) * 0.5f;
+        put3(RP_ARM_BOUND, ctr);
+        o[RP_ARM_BOUND + 3] = sqrtf(dot(half, half)) * 1.0001f + rmax + 1e-4f;
+    }
     for (int ob = 0; ob < 2; ob++) {
         Body bd;
         if (ob < n_objects) load_body(s, i, ob, bd);
@@ -839,13 +860,16 @@ __global__ __launch_bounds__(kRenderBlock) void k_render(RenderArgs a, const flo
                            : ray_box(o, d, c0, R, a.object_half, tmin, h);
             if (hit) role = VR_OBJECT1 + ob;
         }
-        for (int k = 0; k < RENDER_CAPSULES; k++) {
-            const float *q = pr + RP_CAPS + k * 7;
-            if (ray_capsule(o, d, mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), q[6], tmin, h)) role = VR_ROBOT;
-        }
-        for (int k = 0; k < PM_NUM_SPHERES; k++) {
-            const float *q = pr + RP_SPH + k * 4;
-            if (ray_sphere(o, d, mk(q[0], q[1], q[2]), q[3], tmin, h)) role = VR_ROBOT;
+        if (ray_meets_sphere(o, d, mk(pr[RP_ARM_BOUND], pr[RP_ARM_BOUND + 1], pr[RP_ARM_BOUND + 2]),
+                             pr[RP_ARM_BOUND + 3], h.t)) {
+            for (int k = 0; k < RENDER_CAPSULES; k++) {
+                const float *q = pr + RP_CAPS + k * 7;
+                if (ray_capsule(o, d, mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), q[6], tmin, h)) role = VR_ROBOT;
+            }
+            for (int k = 0; k < PM_NUM_SPHERES; k++) {
+                const float *q = pr + RP_SPH + k * 4;
+                if (ray_sphere(o, d, mk(q[0], q[1], q[2]), q[3], tmin, h)) role = VR_ROBOT;
+            }
         }
         float dep = 1.0f;
         const float *col = a.vis.rgba[role];

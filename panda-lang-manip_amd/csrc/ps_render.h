@@ -6,7 +6,7 @@
 //
 // getCameraImage rasterises the URDF meshes; the Panda meshes are not in this
 // image, so the arm is drawn as capsules between its joint frames plus the
-// gripper's contact spheres (DESIGN.md §Rendering).  Table, plane, objects and
+// gripper's contact spheres (DESIGN.md §11).  Table, plane, objects and
 // ghost targets are exact.  Depth follows the OpenGL convention the
 // reference's deprojection assumes: window depth in [0, 1] of the projection
 // matrix, 1 where nothing is hit.
@@ -29,7 +29,8 @@ constexpr int RP_CAPS = 0;
 constexpr int RP_SPH = RP_CAPS + RENDER_CAPSULES * 7;
 constexpr int RP_OBJ = RP_SPH + PM_NUM_SPHERES * 4;
 constexpr int RP_TGT = RP_OBJ + 2 * 12;
-constexpr int RENDER_PRIM_FLOATS = RP_TGT + 2 * 12;
+constexpr int RP_ARM_BOUND = RP_TGT + 2 * 12;  // centre.xyz, radius of a sphere around every arm primitive
+constexpr int RENDER_PRIM_FLOATS = RP_ARM_BOUND + 4;
 
 struct Hit {
     float t;
@@ -94,6 +95,15 @@ PS_D bool ray_cylinder(V3 o, V3 d, V3 c, const M3 &R, float r, float hh, float t
         }
     }
     return got;
+}
+
+// does the ray meet the sphere (c, r) at some t < tmax?  (culling only)
+PS_D bool ray_meets_sphere(V3 o, V3 d, V3 c, float r, float tmax) {
+    V3 oc = o - c;
+    float a = dot(d, d), b = dot(oc, d), cc = dot(oc, oc) - r * r;
+    if (cc <= 0.0f) return true;  // the eye is inside
+    float disc = b * b - a * cc;
+    return disc >= 0.0f && b < 0.0f && (-b - sqrtf(disc)) < tmax * a;
 }
 
 PS_D bool ray_sphere(V3 o, V3 d, V3 c, float r, float tmin, Hit &hit) {

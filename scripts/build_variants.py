@@ -14,6 +14,9 @@ VARIANTS = {
     "maxilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
     "bias0": ["-mllvm", "-amdgpu-schedule-metric-bias=0"],
     "mi_lds": ["-DPS_MI_LDS"],
+    "unroll_off": ["-mllvm", "-amdgpu-unroll-threshold-private=0"],
+    "ilp_min": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
+    "no_early_if": ["-mllvm", "-amdgpu-early-ifcvt=0"],
 }
 
 

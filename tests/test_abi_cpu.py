@@ -113,3 +113,20 @@ def test_no_silent_cpu_fallback():
 
     with pytest.raises(PandasimError):
         make("PandaReach-v3", num_envs=4)
+
+
+def test_bench_algorithmic_bytes_and_pmc_entries():
+    """bench.py's roofline basis: bytes one env-step must
+    move, and the committed per-launch PMC figures it reads."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.algorithmic_bytes_per_env_step(obs_dim=18, action_dim=3) == 658  # PandaPush-v3
+    assert bench.algorithmic_bytes_per_env_step(obs_dim=6, action_dim=3, n_objects=0) == 458  # PandaReach-v3
+    traffic = bench.load_pmc("PandaPush-v3 x65536/gpu")
+    assert traffic is None or traffic > 0
+    valu = bench.load_pmc("PandaPush-v3 x65536/gpu", "valu_insts_per_launch")
+    assert valu is None or valu > 1e8
+    assert bench.load_pmc("no such workload") is None
