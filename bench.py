@@ -88,11 +88,59 @@ def cpu_baseline(task: str, seconds: float):
     v1, _, s1, d1 = run(1, 64, seconds / 3)
     n_env = 16 * threads
     vn, used, sn, dn = run(threads, n_env, seconds * 2 / 3)
+    O.lib().po_set_threads(1)
     return {"value": round(vn, 2), "unit": "env-steps/s", "cores": used, "kind": "port",
-            "value_1core": round(v1, 2),
+            "value_1core": round(v1, 2), "phase_split_1core": cpu_phase_split(O, task),
+            "c1_reach_dense_1env": cpu_reach_dense_1env(O),
             "sample": f"{n_env} envs x {sn} steps of {task} (ee, sparse) in {dn:.1f} s on {used} host threads "
                       f"(OpenMP over envs) + 64 envs x {s1} steps in {d1:.1f} s on 1 thread; fp64 oracle, "
                       f"PyBullet not installed on the box"}
+
+
+def cpu_phase_split(O, task: str, n_env: int = 16, steps: int = 3):
+    """Share of one CPU env-step (fp64 oracle, 1 thread) in Panda.set_action's
+    IK, the 20 substeps and the rest (obs, reward, TimeLimit) -- SURVEY.md §8(d)."""
+    import numpy as np
+
+    cfg = O.config(task)
+    envs = [O.new_env(cfg) for _ in range(n_env)]
+    for i, e in enumerate(envs):
+        O.reset(cfg, e, seed=12345 + i)
+    rng = np.random.default_rng(1)
+    t_step = t_ik = t_sim = 0.0
+    for _ in range(steps):
+        for e in envs:
+            a = rng.uniform(-1, 1, O.action_dim(cfg)).astype(np.float32)
+            t0 = time.perf_counter()
+            pos, _, _, _ = O.link_state(cfg, e, 11)
+            O.inverse_kinematics(cfg, np.array(e.q[:]), 11, pos + 0.05 * a[:3], np.array([1.0, 0.0, 0.0, 0.0]))
+            t1 = time.perf_counter()
+            O.sim_step(cfg, e)
+            t2 = time.perf_counter()
+            O.step(cfg, e, a, autoreset=True)
+            t3 = time.perf_counter()
+            t_ik += t1 - t0
+            t_sim += t2 - t1
+            t_step += t3 - t2
+    k = 1e6 / (n_env * steps)
+    return {"unit": "us per env-step", "step": round(t_step * k, 1), "ik": round(t_ik * k, 1),
+            "substeps": round(t_sim * k, 1), "note": "ik and substeps timed separately on the same states "
+            "(substeps with the previous step's motors); their sum can exceed step by the PGS-iteration spread"}
+
+
+def cpu_reach_dense_1env(O, seconds: float = 1.0):
+    """BASELINE configs[0]: PandaReachDense-v3, 1 env, on the CPU (fp64 oracle)."""
+    import numpy as np
+
+    cfg = O.config("reach", reward="dense")
+    env = O.new_env(cfg)
+    O.reset(cfg, env, seed=12345)
+    rng = np.random.default_rng(0)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        O.step(cfg, env, rng.uniform(-1, 1, 3).astype(np.float32), autoreset=True)
+        n += 1
+    return {"value": round(n / (time.perf_counter() - t0), 1), "unit": "env-steps/s", "cores": 1}
 
 
 def load_pmc(workload: str, key: str = "bytes_per_launch"):
