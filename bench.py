@@ -173,10 +173,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # one process per GPU; the modulo only matters when rehearsing N ranks on
+    # fewer GPUs (PANDASIM_DIST_BACKEND=gloo: RCCL refuses two ranks per GPU)
+    dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("PANDASIM_DIST_BACKEND", "nccl")  # "nccl" is RCCL on ROCm
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import pandasim
     from pandasim.dist import EpisodeStats, gather_to_rank0, max_over_ranks, shard_seeds
