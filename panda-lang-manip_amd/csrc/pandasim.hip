@@ -824,21 +824,21 @@ PS_D M3 m3_at(const float *p) {
 }
 
 // getCameraImage (pybullet.py:186-192) by ray casting: one lane per pixel,
-// blockIdx.y = env.  Pixel (row r, col c) is sampled at its centre, as a
+// blockIdx.x = env.  Pixel (row r, col c) is sampled at its centre, as a
 // rasteriser does; depth is OpenGL window depth of the projection matrix.
 constexpr int kRenderBlock = 256;
 constexpr int kRenderPix = 4;  // pixels per lane (strided by the block)
 
 __global__ __launch_bounds__(kRenderBlock) void k_render(RenderArgs a, const float *prims, float *depth, uint8_t *rgb) {
     __shared__ float pr[RENDER_PRIM_FLOATS];
-    const int64_t env = blockIdx.y;
+    const int64_t env = blockIdx.x;  // x: envs (up to 2^31), y: pixel tiles (<= 65 535)
     for (int k = threadIdx.x; k < RENDER_PRIM_FLOATS; k += kRenderBlock) pr[k] = prims[env * RENDER_PRIM_FLOATS + k];
     __syncthreads();
     const Cam &cm = a.cam;
     const int64_t npix = (int64_t)a.width * a.height;
     const M3 I3 = M3{{1, 0, 0, 0, 1, 0, 0, 0, 1}};
     for (int pp = 0; pp < kRenderPix; pp++) {
-        int64_t pix = ((int64_t)blockIdx.x * kRenderPix + pp) * kRenderBlock + threadIdx.x;
+        int64_t pix = ((int64_t)blockIdx.y * kRenderPix + pp) * kRenderBlock + threadIdx.x;
         if (pix >= npix) break;
         int r = (int)(pix / a.width), c = (int)(pix - (int64_t)r * a.width);
         float xn = -1.0f + (2.0f * c + 1.0f) / a.width, yn = 1.0f - (2.0f * r + 1.0f) / a.height;
@@ -1335,7 +1335,9 @@ int ps_render(ps_ctx *c, const void *state, const float view[16], const float pr
     a.has_plane = c->cfg.has_plane;
     a.vis = *vis;
     int64_t npix = (int64_t)width * height;
-    dim3 g((unsigned)((npix + kRenderBlock * kRenderPix - 1) / (kRenderBlock * kRenderPix)), (unsigned)c->num_envs);
+    int64_t tiles = (npix + kRenderBlock * kRenderPix - 1) / (kRenderBlock * kRenderPix);
+    if (tiles > 65535) return fail(c, PS_ERR_ARG, "image too large (more than 65 535 pixel tiles)");
+    dim3 g((unsigned)c->num_envs, (unsigned)tiles);
     hipLaunchKernelGGL(k_render, g, dim3(kRenderBlock), 0, st, a, c->render_prims, depth, rgb);
     return check_launch(c);
 }

@@ -158,3 +158,19 @@ def test_render_rejects_sizes_the_reference_cannot_stack():
     env.reset(seed=1)
     with pytest.raises(ValueError):
         env.sim.render(width=49, height=64)
+
+
+def test_render_batch_beyond_65535_envs():
+    """Envs ride grid.x: 70 000 envs render, and env 69 999's image equals the
+    image of the same env rendered alone (env i of reset(seed=s) is seeded s + i)."""
+    from pandasim.envs import PandaVecEnv
+
+    big = PandaVecEnv("push", "sparse", "ee", 70000, "cuda:0", autoreset=False)
+    big.reset(seed=100)
+    one = PandaVecEnv("push", "sparse", "ee", 1, "cuda:0", autoreset=False)
+    one.reset(seed=100 + 69999)
+    view, proj, _ = big.sim.get_cam2world_transforms(16, 12, np.zeros(3), 1.4, 45, -30, 0)
+    db, cb = big.sim.get_camera_image(16, 12, view, proj)
+    d1, c1 = one.sim.get_camera_image(16, 12, view, proj)
+    assert torch.equal(db[69999], d1[0]) and torch.equal(cb[69999], c1[0])
+    assert bool((db < 1.0).any())
