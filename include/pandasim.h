@@ -231,7 +231,8 @@ int ps_deproject_image(ps_ctx *ctx, const float *depth, const double tran_pix_wo
                        double *points, uint8_t *valid, double *pixels_2d, void *stream);
 
 /* PyBullet.deproject(depth, pixels, tran_pix_world) (pybullet.py:109-146):
- * n pixels (column, row) int32 per env [B, n, 2] -> points [B, n, 3] f64. */
+ * n pixels (column, row) int32 per env [B, n, 2] -> points [B, n, 3] f64;
+ * a pixel outside the image reads nothing and yields a NaN point. */
 int ps_deproject_pixels(ps_ctx *ctx, const float *depth, const int32_t *pixels, int n,
                         const double tran_pix_world[16], int width, int height, double *points, void *stream);
 

@@ -983,6 +983,11 @@ __global__ __launch_bounds__(256) void k_deproject_pixels(int64_t n_env, int n, 
     if (g >= n_env * n) return;
     int64_t env = g / n;
     int pc = pixels[g * 2 + 0], prow = pixels[g * 2 + 1];
+    if (pc < 0 || pc >= width || prow < 0 || prow >= height) {
+        // outside the image (numpy would raise; the host wrapper does): no read, NaN point
+        points[g * 3 + 0] = points[g * 3 + 1] = points[g * 3 + 2] = __builtin_nan("");
+        return;
+    }
     // x = px * 1 / w (integer numerator, true division), x *= 2, x -= 1; the same for
     // (h - py); z = 2 depth[py, px] - 1
     double x = opaque(opaque((double)pc / (double)width) * 2.0) - 1.0;

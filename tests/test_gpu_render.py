@@ -174,3 +174,21 @@ def test_render_batch_beyond_65535_envs():
     d1, c1 = one.sim.get_camera_image(16, 12, view, proj)
     assert torch.equal(db[69999], d1[0]) and torch.equal(cb[69999], c1[0])
     assert bool((db < 1.0).any())
+
+
+def test_deproject_pixels_out_of_image(sim1):
+    """The host wrapper raises like numpy's indexing; the C ABI itself reads
+    nothing for such a pixel and returns a NaN point."""
+    import ctypes as C
+
+    from pandasim.sim import _ptr
+
+    depth = torch.full((1, 4, 5), 0.5, dtype=torch.float32, device="cuda")
+    with pytest.raises(IndexError):
+        sim1.deproject(depth, [[5, 0]], np.eye(4), width=5, height=4)
+    pix = torch.tensor([[[0, 0], [5, 0], [0, -1], [4, 3]]], dtype=torch.int32, device="cuda")
+    pts = torch.empty(1, 4, 3, dtype=torch.float64, device="cuda")
+    T = (C.c_double * 16)(*np.eye(4).reshape(-1).tolist())
+    sim1._call("ps_deproject_pixels", sim1._ctx, _ptr(depth), _ptr(pix), 4, T, 5, 4, _ptr(pts), sim1._stream())
+    p = pts[0].cpu().numpy()
+    assert np.isfinite(p[[0, 3]]).all() and np.isnan(p[[1, 2]]).all()
