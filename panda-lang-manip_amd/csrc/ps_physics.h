@@ -1101,6 +1101,24 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     float res;
     MJStore L = lds;
 
+    // Row-family gates, fixed for the whole solve: bit k is set when some lane
+    // of the wave has that row.  Taken at the solver's entry (full exec) and
+    // made wave-uniform, so each gate in the loop is a scalar test and branch;
+    // a ballot inside the loop is re-masked by the lanes still iterating and
+    // costs two VALU instructions per row.  Lanes that have converged are
+    // masked off inside a block either way, so the results do not change.
+    auto wave_bits = [&](auto pred, int n) {
+        unsigned m = 0u;
+        for (int k = 0; k < n; k++) m |= __builtin_amdgcn_ballot_w64(pred(k)) ? 1u << k : 0u;
+        return (unsigned)__builtin_amdgcn_readfirstlane((int)m);
+    };
+    const unsigned gate_lim = wave_bits([&](int d) { return ((lim_on >> d) & 1u) != 0u; }, 9);
+    unsigned gate_ground[NB];
+#pragma unroll
+    for (int b = 0; b < NB; b++) gate_ground[b] = wave_bits([&](int c) { return c < ng[b]; }, NG);
+    const unsigned gate_pair = wave_bits([&](int c) { return c < np; }, NP);
+    const unsigned gate_robot = wave_bits([&](int c) { return c < nr; }, NR);
+
     auto joint_row = [&](int d, float sgn, float rhs, float &lam, float lo, float hi) {
         float dl = rhs - dinvj[d] * (sgn * dv[d]);
         float nl = fminf(fmaxf(lam + dl, lo), hi);
@@ -1118,7 +1136,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         res = fmaxf(res, fabsf(x));
     };
     auto limit_row = [&](int d) {
-        if (__builtin_amdgcn_ballot_w64((lim_on >> d) & 1u)) {
+        if (gate_lim & (1u << d)) {
             float sgn = (lim_up >> d) & 1u ? -1.0f : 1.0f;
             float hi = (lim_on >> d) & 1u ? (float)PM_LIMIT_MAX_IMPULSE : 0.0f;
             joint_row(d, sgn, lim_rhs[d], lim_lam[d], 0.0f, hi);
@@ -1151,7 +1169,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             const float inv_m = od[b].inv_m;
 #pragma unroll
             for (int c = 0; c < NG; c++)
-                if (__builtin_amdgcn_ballot_w64(c < ng[b])) {
+                if (gate_ground[b] & (1u << c)) {
                     GroundContact &g = gc[b][c];
                     V3 rn = mk(g.r.y, -g.r.x, 0.0f);  // r x (0,0,1); zero terms dropped below
                     float dl = g.rhs[0] - g.dinv[0] * (rn.x * dw[b].x + rn.y * dw[b].y + dvl[b].z);
@@ -1172,7 +1190,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         if constexpr (NOBJ == 2) {
 #pragma unroll
             for (int c = 0; c < NP; c++)
-                if (__builtin_amdgcn_ballot_w64(c < np)) {
+                if (gate_pair & (1u << c)) {
                     PairContact &p = pc[c];
                     bool A1 = !p.a0;
                     V3 wA = obj_dw(A1), vA = obj_dv(A1), wB = obj_dw(!A1), vB = obj_dv(!A1);
@@ -1190,7 +1208,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         }
 #pragma unroll
         for (int c = 0; c < NR; c++)
-            if (__builtin_amdgcn_ballot_w64(c < nr)) {
+            if (gate_robot & (1u << c)) {
                 RobotContact &r = rc[c];
                 // M^-1 J^T column first: its LDS latency hides under the dot
                 float mj[9];
@@ -1222,7 +1240,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             const float inv_m = od[b].inv_m;
 #pragma unroll
             for (int c = 0; c < NG; c++)
-                if (__builtin_amdgcn_ballot_w64(c < ng[b])) {
+                if (gate_ground[b] & (1u << c)) {
                     GroundContact &g = gc[b][c];
                     V3 r1 = mk(g.r.z, 0.0f, -g.r.x);  // r x (0,-1,0)
                     V3 r2 = mk(0.0f, g.r.z, -g.r.y);  // r x (1,0,0)
@@ -1258,7 +1276,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             const float pmu = sc.fric * sc.fric;
 #pragma unroll
             for (int c = 0; c < NP; c++)
-                if (__builtin_amdgcn_ballot_w64(c < np)) {
+                if (gate_pair & (1u << c)) {
                     PairContact &p = pc[c];
                     bool A1 = !p.a0;
                     V3 wA = obj_dw(A1), vA = obj_dv(A1), wB = obj_dw(!A1), vB = obj_dv(!A1);
@@ -1284,7 +1302,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         }
 #pragma unroll
         for (int c = 0; c < NR; c++)
-            if (__builtin_amdgcn_ballot_w64(c < nr)) {
+            if (gate_robot & (1u << c)) {
                 RobotContact &r = rc[c];
                 float mj1[9], mj2[9];
 #pragma unroll
@@ -1363,7 +1381,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         res = 0.0f;
 #pragma unroll
         for (int d = 8; d >= 0; d--) motor_row(d);
-        if (__builtin_amdgcn_ballot_w64(lim_on != 0u)) {
+        if (gate_lim != 0u) {
 #pragma unroll
             for (int d = 8; d >= 0; d--) limit_row(d);
         }
@@ -1372,7 +1390,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         PS_COUNT_IT();
         L = lds.opaque();
         res = 0.0f;
-        if (__builtin_amdgcn_ballot_w64(lim_on != 0u)) {
+        if (gate_lim != 0u) {
 #pragma unroll
             for (int d = 0; d < 9; d++) limit_row(d);
         }
