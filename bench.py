@@ -92,9 +92,20 @@ def cpu_baseline(task: str, seconds: float):
     return {"value": round(vn, 2), "unit": "env-steps/s", "cores": used, "kind": "port",
             "value_1core": round(v1, 2), "phase_split_1core": cpu_phase_split(O, task),
             "c1_reach_dense_1env": cpu_reach_dense_1env(O),
+            "cpu_model": cpu_model(),
             "sample": f"{n_env} envs x {sn} steps of {task} (ee, sparse) in {dn:.1f} s on {used} host threads "
                       f"(OpenMP over envs) + 64 envs x {s1} steps in {d1:.1f} s on 1 thread; fp64 oracle, "
                       f"PyBullet not installed on the box"}
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def cpu_phase_split(O, task: str, n_env: int = 16, steps: int = 3):
