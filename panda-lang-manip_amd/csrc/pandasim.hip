@@ -827,16 +827,63 @@ PS_D M3 m3_at(const float *p) {
 // blockIdx.x = env.  Pixel (row r, col c) is sampled at its centre, as a
 // rasteriser does; depth is OpenGL window depth of the projection matrix.
 constexpr int kRenderBlock = 256;
-constexpr int kRenderPix = 4;  // pixels per lane (strided by the block)
+constexpr int kRenderPix = 1;  // pixels per lane (strided by the block)
 
-__global__ __launch_bounds__(kRenderBlock) void k_render(RenderArgs a, const float *prims, float *depth, uint8_t *rgb) {
+// (256, 4): four waves per SIMD at <= 128 VGPRs -- a lone wave per SIMD leaves the
+// ray tests' dependent chains exposed
+__global__ __launch_bounds__(kRenderBlock, 4) void k_render(RenderArgs a, const float *prims, float *depth,
+                                                            uint8_t *rgb) {
     __shared__ float pr[RENDER_PRIM_FLOATS];
+    __shared__ float rgba[8 * 4];  // colours by role, indexed per pixel (a kernarg array would go to scratch)
+    __shared__ unsigned arm_mask;
     const int64_t env = blockIdx.x;  // x: envs (up to 2^31), y: pixel tiles (<= 65 535)
     for (int k = threadIdx.x; k < RENDER_PRIM_FLOATS; k += kRenderBlock) pr[k] = prims[env * RENDER_PRIM_FLOATS + k];
+    if (threadIdx.x < 32) rgba[threadIdx.x] = a.vis.rgba[threadIdx.x >> 2][threadIdx.x & 3];
+    if (threadIdx.x == 0) arm_mask = 0u;
     __syncthreads();
     const Cam &cm = a.cam;
     const int64_t npix = (int64_t)a.width * a.height;
+    // Row culling of the arm primitives: this block's pixels span image rows
+    // [r0, r1]; primitive k (capsules, then spheres) joins the mask when its
+    // bounding sphere's conservative projected row range meets them.
+    if (threadIdx.x < RENDER_CAPSULES + PM_NUM_SPHERES) {
+        const int k = threadIdx.x;
+        V3 c;
+        float rad;
+        if (k < RENDER_CAPSULES) {
+            const float *q = pr + RP_CAPS + k * 7;
+            V3 pa = mk(q[0], q[1], q[2]), pb = mk(q[3], q[4], q[5]);
+            c = (pa + pb) * 0.5f;
+            rad = 0.5f * norm(pb - pa) + q[6];
+        } else {
+            const float *q = pr + RP_SPH + (k - RENDER_CAPSULES) * 4;
+            c = mk(q[0], q[1], q[2]);
+            rad = q[3];
+        }
+        rad = rad * 1.001f + 1e-4f;
+        int64_t p0 = (int64_t)blockIdx.y * kRenderPix * kRenderBlock;
+        int64_t p1 = p0 + kRenderPix * kRenderBlock - 1;
+        if (p1 >= npix) p1 = npix - 1;
+        const float r0 = (float)(p0 / a.width), r1 = (float)(p1 / a.width);
+        V3 v = c - cm.eye;
+        float ze = dot(v, cm.f), yu = dot(v, cm.u);
+        bool hit = true;
+        if (ze - rad > cm.nearv) {
+            float dmin = ze - rad, dmax = ze + rad;
+            float nhi = yu + rad, nlo = yu - rad;
+            float yhi = cm.p11 * (nhi >= 0.0f ? nhi / dmin : nhi / dmax);
+            float ylo = cm.p11 * (nlo <= 0.0f ? nlo / dmin : nlo / dmax);
+            // pixel-centre rows: y = 1 - (2 r + 1) / H
+            float rlo = ((1.0f - yhi) * a.height - 1.0f) * 0.5f - 1.0f;
+            float rhi = ((1.0f - ylo) * a.height - 1.0f) * 0.5f + 1.0f;
+            hit = rlo <= r1 && rhi >= r0;
+        }
+        if (hit) atomicOr(&arm_mask, 1u << k);
+    }
+    __syncthreads();
+    const unsigned mask = arm_mask;
     const M3 I3 = M3{{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+#pragma unroll 1
     for (int pp = 0; pp < kRenderPix; pp++) {
         int64_t pix = ((int64_t)blockIdx.y * kRenderPix + pp) * kRenderBlock + threadIdx.x;
         if (pix >= npix) break;
@@ -860,19 +907,21 @@ __global__ __launch_bounds__(kRenderBlock) void k_render(RenderArgs a, const flo
                            : ray_box(o, d, c0, R, a.object_half, tmin, h);
             if (hit) role = VR_OBJECT1 + ob;
         }
-        if (ray_meets_sphere(o, d, mk(pr[RP_ARM_BOUND], pr[RP_ARM_BOUND + 1], pr[RP_ARM_BOUND + 2]),
-                             pr[RP_ARM_BOUND + 3], h.t)) {
+        if (mask && ray_meets_sphere(o, d, mk(pr[RP_ARM_BOUND], pr[RP_ARM_BOUND + 1], pr[RP_ARM_BOUND + 2]),
+                                     pr[RP_ARM_BOUND + 3], h.t)) {
             for (int k = 0; k < RENDER_CAPSULES; k++) {
+                if (!(mask & (1u << k))) continue;
                 const float *q = pr + RP_CAPS + k * 7;
                 if (ray_capsule(o, d, mk(q[0], q[1], q[2]), mk(q[3], q[4], q[5]), q[6], tmin, h)) role = VR_ROBOT;
             }
             for (int k = 0; k < PM_NUM_SPHERES; k++) {
+                if (!(mask & (1u << (RENDER_CAPSULES + k)))) continue;
                 const float *q = pr + RP_SPH + k * 4;
                 if (ray_sphere(o, d, mk(q[0], q[1], q[2]), q[3], tmin, h)) role = VR_ROBOT;
             }
         }
         float dep = 1.0f;
-        const float *col = a.vis.rgba[role];
+        const float *col = rgba + role * 4;
         float cr = col[0], cg = col[1], cb = col[2];
         if (role != VR_BACKGROUND) {
             float ze = -h.t;
@@ -896,7 +945,7 @@ __global__ __launch_bounds__(kRenderBlock) void k_render(RenderArgs a, const flo
                        : shape == PS_VISUAL_SPHERE ? ray_sphere(o, d, c0, hh.x, tmin, gh)
                                                    : ray_box(o, d, c0, R, hh, tmin, gh);
             if (hit) {
-                const float *tc = a.vis.rgba[VR_TARGET1 + g];
+                const float *tc = rgba + (VR_TARGET1 + g) * 4;
                 float al = tc[3];
                 cr = al * tc[0] + (1.0f - al) * cr;
                 cg = al * tc[1] + (1.0f - al) * cg;

@@ -37,6 +37,10 @@ struct Hit {
     V3 n;
 };
 
+// v_rcp_f32 (1 ulp): the ray tests only need image-quality reciprocals, and the
+// IEEE division would cost ten instructions each
+PS_D float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
 // slab test of the ray (o, d) against the box of half extents h centred at c
 // with rotation R (columns = box axes); t in [tmin, t.t) updates the hit
 PS_D bool ray_box(V3 o, V3 d, V3 c, const M3 &R, V3 h, float tmin, Hit &hit) {
@@ -47,7 +51,7 @@ PS_D bool ray_box(V3 o, V3 d, V3 c, const M3 &R, V3 h, float tmin, Hit &hit) {
     const float oo[3] = {lo.x, lo.y, lo.z}, dd[3] = {ld.x, ld.y, ld.z}, hh[3] = {h.x, h.y, h.z};
 #pragma unroll
     for (int k = 0; k < 3; k++) {
-        float inv = 1.0f / dd[k];  // +-inf for an axis-parallel ray: the slab test still holds
+        float inv = frcp(dd[k]);  // +-inf for an axis-parallel ray: the slab test still holds
         float ta = (-hh[k] - oo[k]) * inv, tb = (hh[k] - oo[k]) * inv;
         float tn = fminf(ta, tb), tf = fmaxf(ta, tb);
         if (tn > t0) {
@@ -59,7 +63,9 @@ PS_D bool ray_box(V3 o, V3 d, V3 c, const M3 &R, V3 h, float tmin, Hit &hit) {
     }
     if (!(t0 <= t1) || t0 < tmin || t0 >= hit.t) return false;
     hit.t = t0;
-    hit.n = col(R, ax) * sg;
+    // selects, not col(R, ax): a runtime column index would send R to scratch
+    V3 n = ax == 0 ? mk(R.m[0], R.m[3], R.m[6]) : ax == 1 ? mk(R.m[1], R.m[4], R.m[7]) : mk(R.m[2], R.m[5], R.m[8]);
+    hit.n = n * sg;
     return true;
 }
 
@@ -72,11 +78,12 @@ PS_D bool ray_cylinder(V3 o, V3 d, V3 c, const M3 &R, float r, float hh, float t
         float b = lo.x * ld.x + lo.y * ld.y, cc = lo.x * lo.x + lo.y * lo.y - r * r;
         float disc = b * b - a * cc;
         if (disc >= 0.0f) {
-            float t = (-b - sqrtf(disc)) / a;
+            float t = (-b - sqrtf(disc)) * frcp(a);
             float z = lo.z + t * ld.z;
             if (t >= tmin && t < hit.t && fabsf(z) <= hh) {
                 hit.t = t;
-                hit.n = mul(R, mk((lo.x + t * ld.x) / r, (lo.y + t * ld.y) / r, 0.0f));
+                float ir = frcp(r);
+                hit.n = mul(R, mk((lo.x + t * ld.x) * ir, (lo.y + t * ld.y) * ir, 0.0f));
                 got = true;
             }
         }
@@ -85,7 +92,7 @@ PS_D bool ray_cylinder(V3 o, V3 d, V3 c, const M3 &R, float r, float hh, float t
 #pragma unroll
         for (int s = 0; s < 2; s++) {
             float zc = s ? hh : -hh;
-            float t = (zc - lo.z) / ld.z;
+            float t = (zc - lo.z) * frcp(ld.z);
             float x = lo.x + t * ld.x, y = lo.y + t * ld.y;
             if (t >= tmin && t < hit.t && x * x + y * y <= r * r) {
                 hit.t = t;
@@ -111,11 +118,11 @@ PS_D bool ray_sphere(V3 o, V3 d, V3 c, float r, float tmin, Hit &hit) {
     float a = dot(d, d), b = dot(oc, d), cc = dot(oc, oc) - r * r;
     float disc = b * b - a * cc;
     if (disc < 0.0f) return false;
-    float t = (-b - sqrtf(disc)) / a;
+    float t = (-b - sqrtf(disc)) * frcp(a);
     if (t < tmin || t >= hit.t) return false;
     hit.t = t;
     V3 p = oc + d * t;
-    hit.n = p * (1.0f / r);
+    hit.n = p * frcp(r);
     return true;
 }
 
@@ -127,7 +134,7 @@ PS_D bool ray_capsule(V3 o, V3 d, V3 pa, V3 pb, float r, float tmin, Hit &hit) {
     float a = baba * dd - bard * bard, b = baba * rdoa - baoa * bard, c = baba * oaoa - baoa * baoa - r * r * baba;
     float h = b * b - a * c;
     if (h < 0.0f) return false;
-    float t = (-b - sqrtf(h)) / a;
+    float t = (-b - sqrtf(h)) * frcp(a);
     float y = baoa + t * bard;
     if (!(y > 0.0f && y < baba)) {
         // caps
@@ -136,14 +143,14 @@ PS_D bool ray_capsule(V3 o, V3 d, V3 pa, V3 pb, float r, float tmin, Hit &hit) {
         c = dot(oc, oc) - r * r;
         h = b * b - dd * c;
         if (h < 0.0f) return false;
-        t = (-b - sqrtf(h)) / dd;
+        t = (-b - sqrtf(h)) * frcp(dd);
     }
     if (!(t >= tmin && t < hit.t)) return false;
     V3 p = o + d * t - pa;
-    float s = fminf(fmaxf(dot(p, ba) / baba, 0.0f), 1.0f);
+    float s = fminf(fmaxf(dot(p, ba) * frcp(baba), 0.0f), 1.0f);
     V3 n = p - ba * s;
     hit.t = t;
-    hit.n = n * (1.0f / r);
+    hit.n = n * frcp(r);
     return true;
 }
 
