@@ -195,7 +195,7 @@ class RobotTaskEnv:
     truncation is TimeLimit's job), info).
     """
 
-    metadata = {"render_modes": []}
+    metadata = {"render_modes": ["rgb_array"]}
 
     def __init__(self, robot: PyBulletRobot, task: Task) -> None:
         assert robot.sim == task.sim, "The robot and the task must belong to the same simulation."
@@ -266,9 +266,18 @@ class RobotTaskEnv:
     def close(self) -> None:
         self.sim.close()
 
-    def render(self, *args, **kwargs):
-        """core.py:291-335 (broken in the reference: SURVEY.md §5); out of scope."""
-        raise NotImplementedError("rendering is outside this path (SURVEY.md §8(f) rank 4)")
+    def render(self, mode: str = "human", width: int = 720, height: int = 480, target_position=None,
+               distance: float = 1.4, yaw: float = 45, pitch: float = -30, roll: float = 0):
+        """core.py:294-335.  The reference passes `mode` positionally into
+        PyBullet.render's `width` (pybullet.py:149), so it cannot run; this
+        returns what its docstring promises: "rgb_array" -> [B, height, width, 3]
+        uint8 RGB of every env (getCameraImage), "human" -> None
+        (there is no window)."""
+        if mode != "rgb_array":
+            return None
+        target_position = np.zeros(3) if target_position is None else target_position
+        view, proj, _ = self.sim.get_cam2world_transforms(width, height, target_position, distance, yaw, pitch, roll)
+        return self.sim.get_camera_image(width, height, view, proj)[1]
 
 
 class TimeLimit:

@@ -40,7 +40,7 @@ def _spaces(obs_dim: int, action_dim: int, goal_dim: int = 3):
 
 
 class PandaVecEnv:
-    metadata = {"render_modes": []}
+    metadata = {"render_modes": ["rgb_array"]}
 
     def __init__(self, task: str, reward_type: str = "sparse", control_type: str = "ee", num_envs: int = 1,
                  device="cuda", autoreset: bool = True):
@@ -141,6 +141,16 @@ class PandaVecEnv:
     def remove_state(self, state_id: int) -> None:
         self._saved_goals.pop(state_id, None)
         self.sim.remove_state(state_id)
+
+    def render(self, mode: str = "rgb_array", width: int = 720, height: int = 480, target_position=None,
+               distance: float = 1.4, yaw: float = 45, pitch: float = -30, roll: float = 0):
+        """RobotTaskEnv.render (core.py:294-335) for every env: "rgb_array" ->
+        [B, height, width, 3] uint8; "human" -> None."""
+        if mode != "rgb_array":
+            return None
+        target_position = np.zeros(3) if target_position is None else target_position
+        view, proj, _ = self.sim.get_cam2world_transforms(width, height, target_position, distance, yaw, pitch, roll)
+        return self.sim.get_camera_image(width, height, view, proj)[1]
 
     def close(self) -> None:
         self.sim.close()

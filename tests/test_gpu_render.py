@@ -192,3 +192,18 @@ def test_deproject_pixels_out_of_image(sim1):
     sim1._call("ps_deproject_pixels", sim1._ctx, _ptr(depth), _ptr(pix), 4, T, 5, 4, _ptr(pts), sim1._stream())
     p = pts[0].cpu().numpy()
     assert np.isfinite(p[[0, 3]]).all() and np.isnan(p[[1, 2]]).all()
+
+
+def test_env_render_rgb_array():
+    """RobotTaskEnv.render (core.py:294-335) through both env paths."""
+    import pandasim
+
+    env = pandasim.make("PandaPush-v3", num_envs=3)
+    env.reset(seed=0)
+    img = env.render("rgb_array", width=64, height=48)
+    assert img.shape == (3, 48, 64, 3) and img.dtype == torch.uint8
+    assert env.render("human") is None
+    plug = pandasim.make("PandaPush-v3", num_envs=3, fused=False)
+    plug.reset(seed=0)
+    img2 = plug.env.render("rgb_array", width=64, height=48)
+    assert img2.shape == (3, 48, 64, 3)
