@@ -474,3 +474,25 @@ def test_gripper_object_contact_parity(ps, task):
     assert np.mean(moved > 1e-3) > 0.5  # the gripper did reach the objects
     assert (e_obj < 1e-3).mean() >= 0.95 and (e_q < SIM_TIGHT["q"] * 10).mean() >= 0.95
     assert e_obj.max() < 2e-2 and e_q.max() < SIM_LOOSE["q"] * 5
+
+
+@pytest.mark.parametrize("B", [1, 70])
+def test_ragged_batch_parity(ps, B):
+    """Batches that are not a multiple of the 64-lane wave (one env; 70 = a
+    full wave plus a 6-lane one): every env, including the ragged wave's,
+    steps like the oracle from the same state."""
+    env = make_env(ps, "push", "ee", B)
+    env.autoreset = False
+    env.reset(seed=4242)
+    cfg = oracle_config_for(env.sim.cfg)
+    rng = np.random.default_rng(11)
+    groups = _groups("push", 6)
+    for _ in range(3):
+        snap = snapshot(env.sim)
+        a = rng.uniform(-1, 1, size=(B, env.action_dim)).astype(np.float32)
+        obs, *_ = env.step(torch.from_numpy(a).cuda())
+        og = obs["observation"].cpu().numpy()
+        for i in sorted({0, B - 1, B // 2}):
+            o, *_ = O.step(cfg, oracle_env_from(cfg, snap, i), a[i])
+            for k, idx in groups.items():
+                assert np.abs(og[i, idx] - o[idx]).max() <= TOL["push"][k], (B, i, k)
