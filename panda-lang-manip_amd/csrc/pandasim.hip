@@ -488,7 +488,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
         store_motors(s, i, m);
     }
     PS_PHASE(6);
-    __shared__ float smem[LDS_FLOATS * kBlock];
+    __shared__ float smem[lds_floats<T::NOBJ>() * kBlock];
     MJStore lds{(lds_float *)(smem + threadIdx.x), kBlock};
     run_substeps<T::NOBJ, T::SHAPE, true>(P, i, PM_SUBSTEPS, q, qd, bd, lds PS_PROF_ARG);
     double g[6] = {0, 0, 0, 0, 0, 0};
@@ -538,7 +538,7 @@ __global__ __launch_bounds__(kBlock) void k_sim_step(KParams P, int n_substeps) 
     Body bd[NOBJ > 0 ? NOBJ : 1];
 #pragma unroll
     for (int b = 0; b < NOBJ; b++) load_body(s, i, b, bd[b]);
-    __shared__ float smem[LDS_FLOATS * kBlock];
+    __shared__ float smem[lds_floats<NOBJ>() * kBlock];
     MJStore lds{(lds_float *)(smem + threadIdx.x), kBlock};
 #ifdef PS_PROFILE_PHASES
     PhaseTimer pt;

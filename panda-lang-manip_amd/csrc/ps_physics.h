@@ -553,6 +553,19 @@ constexpr int LDS_FLOATS = LDS_MI_OFFSET + 45;
 #else
 constexpr int LDS_FLOATS = LDS_MI_OFFSET;
 #endif
+// Stack (two cubes) also keeps the read-only data of the second cube's ground
+// rows (r, rhs, dinv: 9 per contact) and of the box-box pair rows (dir, rA x
+// dir, rB x dir, rhs, dinv: 33 per contact) in LDS: in registers they spilled
+// ~1.8 KB per lane to scratch beyond L2.  316 floats per lane = 79 KB per
+// 64-lane workgroup, i.e. two workgroups per CU (two rounds of 65 536 envs).
+constexpr int LDS_GND_OFFSET = LDS_MI_OFFSET;
+constexpr int LDS_GND_FLOATS = 9;
+constexpr int LDS_PAIR_OFFSET = LDS_GND_OFFSET + NG * LDS_GND_FLOATS;
+constexpr int LDS_PAIR_FLOATS = 33;
+constexpr int LDS_FLOATS_STACK = LDS_PAIR_OFFSET + NP * LDS_PAIR_FLOATS;
+static_assert(LDS_FLOATS_STACK * 4 * 64 * 2 <= 160 * 1024, "two Stack workgroups per CU");
+template <int NOBJ>
+constexpr int lds_floats() { return NOBJ == 2 ? LDS_FLOATS_STACK : LDS_FLOATS; }
 
 // object-ground contact: object-only rows; normal +z, friction dirs of
 // planeSpace(+z) = (0,-1,0), (1,0,0).  The cylinder's I^-1 (r x dir) is rebuilt
@@ -586,6 +599,10 @@ struct MJStore {
     PS_D lds_float &at(int slot, int row, int k) const { return base[((slot * 3 + row) * 9 + k) * stride]; }
     PS_D lds_float &mi(int k) const { return base[(LDS_MI_OFFSET + k) * stride]; }
     PS_D lds_float &stash(int k) const { return base[(LDS_STASH_OFFSET + k) * stride]; }
+    // Stack only: second cube's ground row c, field k (r.xyz, rhs[3], dinv[3])
+    PS_D lds_float &gnd(int c, int k) const { return base[(LDS_GND_OFFSET + c * LDS_GND_FLOATS + k) * stride]; }
+    // Stack only: pair row c, field k (dir[3].xyz, rnA[3].xyz, rnB[3].xyz, rhs[3], dinv[3])
+    PS_D lds_float &pair(int c, int k) const { return base[(LDS_PAIR_OFFSET + c * LDS_PAIR_FLOATS + k) * stride]; }
     // a copy whose address the compiler cannot see through: loads from it are
     // not loop-invariant, so they stay in the PGS loop as ds_reads instead of
     // being hoisted into (spilled) registers
@@ -871,6 +888,13 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             gc[b][s] = GroundContact{mk(0, 0, 0), {0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
     }
     const float gmu = sc.fric * (float)PM_DEFAULT_FRICTION;
+    if constexpr (NOBJ == 2) {
+        // unused LDS rows of the second cube must be all-zero no-ops
+#pragma unroll
+        for (int c = 0; c < NG; c++)
+#pragma unroll
+            for (int k = 0; k < LDS_GND_FLOATS; k++) lds.gnd(c, k) = 0.0f;
+    }
 #pragma unroll
     for (int b = 0; b < NOBJ; b++) {
         static_for<0, num_support<SHAPE>()>([&](auto VV) {
@@ -895,9 +919,20 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         g.lam[j] = 0.0f;
                         g.rhs[j] = j == 0 ? normal_rhs(dist, rel, g.dinv[0]) : -rel * g.dinv[j];
                     }
+                    if (NOBJ == 2 && b == 1) {
+                        // Stack: the second cube's read-only row data live in LDS
+                        const int at = ng[b];
+                        lds.gnd(at, 0) = g.r.x; lds.gnd(at, 1) = g.r.y; lds.gnd(at, 2) = g.r.z;
 #pragma unroll
-                    for (int s = 0; s < NG; s++)
-                        if (s == ng[b]) gc[b][s] = g;
+                        for (int j = 0; j < 3; j++) {
+                            lds.gnd(at, 3 + j) = g.rhs[j];
+                            lds.gnd(at, 6 + j) = g.dinv[j];
+                        }
+                    } else {
+#pragma unroll
+                        for (int s = 0; s < NG; s++)
+                            if (s == ng[b]) gc[b][s] = g;
+                    }
                     ng[b]++;
                 }
             }
@@ -944,6 +979,17 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     p.dir[j] = p.rnA[j] = p.rnB[j] = mk(0, 0, 0);
                     p.rhs[j] = p.lam[j] = p.dinv[j] = 0.0f;
                 }
+            }
+            // the read-only part of the row goes to LDS (LDS_PAIR_FLOATS)
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                lds.pair(c, 3 * j + 0) = p.dir[j].x; lds.pair(c, 3 * j + 1) = p.dir[j].y; lds.pair(c, 3 * j + 2) = p.dir[j].z;
+                lds.pair(c, 9 + 3 * j + 0) = p.rnA[j].x; lds.pair(c, 9 + 3 * j + 1) = p.rnA[j].y;
+                lds.pair(c, 9 + 3 * j + 2) = p.rnA[j].z;
+                lds.pair(c, 18 + 3 * j + 0) = p.rnB[j].x; lds.pair(c, 18 + 3 * j + 1) = p.rnB[j].y;
+                lds.pair(c, 18 + 3 * j + 2) = p.rnB[j].z;
+                lds.pair(c, 27 + j) = p.rhs[j];
+                lds.pair(c, 30 + j) = p.dinv[j];
             }
         }
     }
@@ -1167,8 +1213,15 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             for (int c = 0; c < NG; c++)
                 if (gate_ground[b] & (1u << c)) {
                     GroundContact &g = gc[b][c];
-                    V3 rn = mk(g.r.y, -g.r.x, 0.0f);  // r x (0,0,1); zero terms dropped below
-                    float dl = g.rhs[0] - g.dinv[0] * (rn.x * dw[b].x + rn.y * dw[b].y + dvl[b].z);
+                    V3 gr = g.r;
+                    float grhs = g.rhs[0], gdinv = g.dinv[0];
+                    if (NOBJ == 2 && b == 1) {  // Stack's second cube: row data in LDS
+                        gr = mk(L.gnd(c, 0), L.gnd(c, 1), L.gnd(c, 2));
+                        grhs = L.gnd(c, 3);
+                        gdinv = L.gnd(c, 6);
+                    }
+                    V3 rn = mk(gr.y, -gr.x, 0.0f);  // r x (0,0,1); zero terms dropped below
+                    float dl = grhs - gdinv * (rn.x * dw[b].x + rn.y * dw[b].y + dvl[b].z);
                     float nl = fminf(fmaxf(g.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
                     dl = nl - g.lam[0];
                     g.lam[0] = nl;
@@ -1181,7 +1234,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         dw[b].y = fmaf(rn.y, dI, dw[b].y);
                     }
                     dvl[b].z = fmaf(dl, inv_m, dvl[b].z);
-                    res = fmaxf(res, fabsf(dl * res_scale(g.dinv[0])));
+                    res = fmaxf(res, fabsf(dl * res_scale(gdinv)));
                 }
         }
         if constexpr (NOBJ == 2) {
@@ -1189,18 +1242,20 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             for (int c = 0; c < NP; c++)
                 if (gate_pair & (1u << c)) {
                     PairContact &p = pc[c];
+                    // Stack: the row's read-only data come from LDS (LDS_PAIR_FLOATS)
+                    auto pv = [&](int k) { return mk(L.pair(c, k), L.pair(c, k + 1), L.pair(c, k + 2)); };
                     bool A1 = !p.a0;
                     V3 wA = obj_dw(A1), vA = obj_dv(A1), wB = obj_dw(!A1), vB = obj_dv(!A1);
-                    float jv = dot(p.rnA[0], wA) + dot(p.dir[0], vA) - dot(p.rnB[0], wB) - dot(p.dir[0], vB);
-                    float dl = p.rhs[0] - p.dinv[0] * jv;
+                    float jv = dot(pv(9), wA) + dot(pv(0), vA) - dot(pv(18), wB) - dot(pv(0), vB);
+                    float dl = (float)L.pair(c, 27) - (float)L.pair(c, 30) * jv;
                     float nl = fminf(fmaxf(p.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
                     dl = nl - p.lam[0];
                     p.lam[0] = nl;
                     float iIA = A1 ? od[NB - 1].iI : od[0].iI, iIB = A1 ? od[0].iI : od[NB - 1].iI;
                     float imA = A1 ? od[NB - 1].inv_m : od[0].inv_m, imB = A1 ? od[0].inv_m : od[NB - 1].inv_m;
-                    obj_add(A1, p.rnA[0] * (dl * iIA), p.dir[0] * (dl * imA));
-                    obj_add(!A1, p.rnB[0] * (-dl * iIB), p.dir[0] * (-dl * imB));
-                    res = fmaxf(res, fabsf(dl * res_scale(p.dinv[0])));
+                    obj_add(A1, pv(9) * (dl * iIA), pv(0) * (dl * imA));
+                    obj_add(!A1, pv(18) * (-dl * iIB), pv(0) * (-dl * imB));
+                    res = fmaxf(res, fabsf(dl * res_scale((float)L.pair(c, 30))));
                 }
         }
 #pragma unroll
@@ -1239,10 +1294,19 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             for (int c = 0; c < NG; c++)
                 if (gate_ground[b] & (1u << c)) {
                     GroundContact &g = gc[b][c];
-                    V3 r1 = mk(g.r.z, 0.0f, -g.r.x);  // r x (0,-1,0)
-                    V3 r2 = mk(0.0f, g.r.z, -g.r.y);  // r x (1,0,0)
-                    float dla = g.rhs[1] - g.dinv[1] * (r1.x * dw[b].x + r1.z * dw[b].z - dvl[b].y);
-                    float dlb = g.rhs[2] - g.dinv[2] * (r2.y * dw[b].y + r2.z * dw[b].z + dvl[b].x);
+                    V3 gr = g.r;
+                    float grhs1 = g.rhs[1], grhs2 = g.rhs[2], gdinv1 = g.dinv[1], gdinv2 = g.dinv[2];
+                    if (NOBJ == 2 && b == 1) {  // Stack's second cube: row data in LDS
+                        gr = mk(L.gnd(c, 0), L.gnd(c, 1), L.gnd(c, 2));
+                        grhs1 = L.gnd(c, 4);
+                        grhs2 = L.gnd(c, 5);
+                        gdinv1 = L.gnd(c, 7);
+                        gdinv2 = L.gnd(c, 8);
+                    }
+                    V3 r1 = mk(gr.z, 0.0f, -gr.x);  // r x (0,-1,0)
+                    V3 r2 = mk(0.0f, gr.z, -gr.y);  // r x (1,0,0)
+                    float dla = grhs1 - gdinv1 * (r1.x * dw[b].x + r1.z * dw[b].z - dvl[b].y);
+                    float dlb = grhs2 - gdinv2 * (r2.y * dw[b].y + r2.z * dw[b].z + dvl[b].x);
                     float sa = g.lam[1] + dla, sb = g.lam[2] + dlb;
                     float lim = gmu * fmaxf(g.lam[0], 0.0f);
                     float m2 = sa * sa + sb * sb;
@@ -1265,7 +1329,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     }
                     dvl[b].x = fmaf(dlb, inv_m, dvl[b].x);
                     dvl[b].y = fmaf(-dla, inv_m, dvl[b].y);
-                    res = fmaxf(res, fmaxf(fabsf(dla * res_scale(g.dinv[1])), fabsf(dlb * res_scale(g.dinv[2]))));
+                    res = fmaxf(res, fmaxf(fabsf(dla * res_scale(gdinv1)), fabsf(dlb * res_scale(gdinv2))));
                 }
         }
         if constexpr (NOBJ == 2) {
@@ -1274,11 +1338,13 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             for (int c = 0; c < NP; c++)
                 if (gate_pair & (1u << c)) {
                     PairContact &p = pc[c];
+                    // Stack: the row's read-only data come from LDS (LDS_PAIR_FLOATS)
+                    auto pv = [&](int k) { return mk(L.pair(c, k), L.pair(c, k + 1), L.pair(c, k + 2)); };
                     bool A1 = !p.a0;
                     V3 wA = obj_dw(A1), vA = obj_dv(A1), wB = obj_dw(!A1), vB = obj_dv(!A1);
-                    float ja = dot(p.rnA[1], wA) + dot(p.dir[1], vA) - dot(p.rnB[1], wB) - dot(p.dir[1], vB);
-                    float jb = dot(p.rnA[2], wA) + dot(p.dir[2], vA) - dot(p.rnB[2], wB) - dot(p.dir[2], vB);
-                    float dla = p.rhs[1] - p.dinv[1] * ja, dlb = p.rhs[2] - p.dinv[2] * jb;
+                    float ja = dot(pv(12), wA) + dot(pv(3), vA) - dot(pv(21), wB) - dot(pv(3), vB);
+                    float jb = dot(pv(15), wA) + dot(pv(6), vA) - dot(pv(24), wB) - dot(pv(6), vB);
+                    float dla = (float)L.pair(c, 28) - (float)L.pair(c, 31) * ja, dlb = (float)L.pair(c, 29) - (float)L.pair(c, 32) * jb;
                     float sa = p.lam[1] + dla, sb = p.lam[2] + dlb;
                     float lim = pmu * fmaxf(p.lam[0], 0.0f);
                     float m2 = sa * sa + sb * sb;
@@ -1291,9 +1357,9 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     p.lam[2] = sb;
                     float iIA = A1 ? od[NB - 1].iI : od[0].iI, iIB = A1 ? od[0].iI : od[NB - 1].iI;
                     float imA = A1 ? od[NB - 1].inv_m : od[0].inv_m, imB = A1 ? od[0].inv_m : od[NB - 1].inv_m;
-                    obj_add(A1, (p.rnA[1] * dla + p.rnA[2] * dlb) * iIA, (p.dir[1] * dla + p.dir[2] * dlb) * imA);
-                    obj_add(!A1, (p.rnB[1] * dla + p.rnB[2] * dlb) * -iIB, (p.dir[1] * dla + p.dir[2] * dlb) * -imB);
-                    res = fmaxf(res, fmaxf(fabsf(dla * res_scale(p.dinv[1])), fabsf(dlb * res_scale(p.dinv[2]))));
+                    obj_add(A1, (pv(12) * dla + pv(15) * dlb) * iIA, (pv(3) * dla + pv(6) * dlb) * imA);
+                    obj_add(!A1, (pv(21) * dla + pv(24) * dlb) * -iIB, (pv(3) * dla + pv(6) * dlb) * -imB);
+                    res = fmaxf(res, fmaxf(fabsf(dla * res_scale((float)L.pair(c, 31))), fabsf(dlb * res_scale((float)L.pair(c, 32)))));
                 }
         }
 #pragma unroll
