@@ -21,6 +21,7 @@ struct ps_ctx {
     int device;
     char err[256];
     float *render_prims;  // [B][RENDER_PRIM_FLOATS] scratch of ps_render, allocated on first use
+    float *gstash;        // Stack: [LDS_STASH_FLOATS][stride] substep stash, allocated on first step
 };
 
 #ifdef PS_PROFILE_PHASES
@@ -86,6 +87,7 @@ struct KParams {
     int64_t n;
     Scene sc;
     int reward_type, block_gripper, obs_dim, action_dim, autoreset;
+    float *gstash;  // Stack: [LDS_STASH_FLOATS][stride] per-substep stash (ctx scratch)
 };
 
 Scene scene_of(const ps_config &c) {
@@ -490,6 +492,10 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
     PS_PHASE(6);
     __shared__ float smem[lds_floats<T::NOBJ>() * kBlock];
     MJStore lds{(lds_float *)(smem + threadIdx.x), kBlock};
+    if constexpr (T::NOBJ == 2) {
+        lds.gst = P.gstash + i;
+        lds.gst_stride = s.stride;
+    }
     run_substeps<T::NOBJ, T::SHAPE, true>(P, i, PM_SUBSTEPS, q, qd, bd, lds PS_PROF_ARG);
     double g[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -540,6 +546,10 @@ __global__ __launch_bounds__(kBlock) void k_sim_step(KParams P, int n_substeps) 
     for (int b = 0; b < NOBJ; b++) load_body(s, i, b, bd[b]);
     __shared__ float smem[lds_floats<NOBJ>() * kBlock];
     MJStore lds{(lds_float *)(smem + threadIdx.x), kBlock};
+    if constexpr (NOBJ == 2) {
+        lds.gst = P.gstash + i;
+        lds.gst_stride = s.stride;
+    }
 #ifdef PS_PROFILE_PHASES
     PhaseTimer pt;
     pt.last = __builtin_amdgcn_s_memtime();
@@ -1074,7 +1084,19 @@ KParams params_of(ps_ctx *c, void *state) {
     P.obs_dim = ps_obs_dim(c);
     P.action_dim = ps_action_dim(c);
     P.autoreset = 0;
+    P.gstash = c->gstash;
     return P;
+}
+
+// Stack's global stash (the LDS it would use holds its ground rows): one
+// allocation on the first step of a two-object context, never per step
+int ensure_stash(ps_ctx *c) {
+    if (c->cfg.n_objects != 2 || c->gstash) return PS_OK;
+    if (hipMalloc((void **)&c->gstash, sizeof(float) * LDS_STASH_FLOATS * c->lay.stride) != hipSuccess) {
+        c->gstash = nullptr;
+        return PS_ERR_HIP;
+    }
+    return PS_OK;
 }
 
 dim3 grid_of(int64_t n, int block) { return dim3((unsigned)((n + block - 1) / block)); }
@@ -1165,6 +1187,7 @@ int ps_create(const ps_config *cfg, int64_t num_envs, int device, ps_ctx **out) 
 
 void ps_destroy(ps_ctx *ctx) {
     if (ctx && ctx->render_prims) (void)hipFree(ctx->render_prims);
+    if (ctx && ctx->gstash) (void)hipFree(ctx->gstash);
     delete ctx;
 }
 
@@ -1223,6 +1246,7 @@ int ps_step(ps_ctx *c, void *state, const float *actions, float *obs, float *ag,
     if (!c || !state || !actions || !reward || !terminated || !truncated)
         return fail(c, PS_ERR_ARG, "null argument");
     if (!scene_matches_task(c->cfg)) return fail(c, PS_ERR_UNSUPPORTED, "scene does not match the task");
+    if (ensure_stash(c) != PS_OK) return fail(c, PS_ERR_HIP, "hipMalloc of the Stack stash failed");
     KParams P = params_of(c, state);
     P.autoreset = autoreset;
     dim3 g = grid_of(P.n, kBlock), b(kBlock);
@@ -1251,6 +1275,7 @@ int ps_step(ps_ctx *c, void *state, const float *actions, float *obs, float *ag,
 
 int ps_sim_step(ps_ctx *c, void *state, int n_substeps, void *stream) {
     if (!c || !state || n_substeps < 0) return fail(c, PS_ERR_ARG, "bad argument");
+    if (ensure_stash(c) != PS_OK) return fail(c, PS_ERR_HIP, "hipMalloc of the Stack stash failed");
     KParams P = params_of(c, state);
     dim3 g = grid_of(P.n, kBlock), b(kBlock);
     hipStream_t st = (hipStream_t)stream;

@@ -553,14 +553,16 @@ constexpr int LDS_FLOATS = LDS_MI_OFFSET + 45;
 #else
 constexpr int LDS_FLOATS = LDS_MI_OFFSET;
 #endif
-// Stack (two cubes) also keeps the read-only data of the second cube's ground
-// rows (r, rhs, dinv: 9 per contact) and of the box-box pair rows (dir, rA x
-// dir, rB x dir, rhs, dinv: 33 per contact) in LDS: in registers they spilled
-// ~1.8 KB per lane to scratch beyond L2.  316 floats per lane = 79 KB per
-// 64-lane workgroup, i.e. two workgroups per CU (two rounds of 65 536 envs).
-constexpr int LDS_GND_OFFSET = LDS_MI_OFFSET;
+// Stack (two cubes) keeps the read-only data of both cubes' ground rows (r,
+// rhs, dinv: 9 per contact) and of the box-box pair rows (dir, rA x dir,
+// rB x dir, rhs, dinv: 33 per contact) in LDS instead of registers, where they
+// spilled ~1.8 KB per lane to scratch beyond L2.  Its 40-float stash moves to a
+// global per-env buffer (written once and read once per substep, L2-resident)
+// and the ground rows take its LDS place: 312 floats per lane = 78 KB per
+// 64-lane workgroup, two workgroups per CU (two rounds of 65 536 envs).
+constexpr int LDS_GND_OFFSET = LDS_STASH_OFFSET;
 constexpr int LDS_GND_FLOATS = 9;
-constexpr int LDS_PAIR_OFFSET = LDS_GND_OFFSET + NG * LDS_GND_FLOATS;
+constexpr int LDS_PAIR_OFFSET = LDS_GND_OFFSET + 2 * NG * LDS_GND_FLOATS;
 constexpr int LDS_PAIR_FLOATS = 33;
 constexpr int LDS_FLOATS_STACK = LDS_PAIR_OFFSET + NP * LDS_PAIR_FLOATS;
 static_assert(LDS_FLOATS_STACK * 4 * 64 * 2 <= 160 * 1024, "two Stack workgroups per CU");
@@ -599,7 +601,11 @@ struct MJStore {
     PS_D lds_float &at(int slot, int row, int k) const { return base[((slot * 3 + row) * 9 + k) * stride]; }
     PS_D lds_float &mi(int k) const { return base[(LDS_MI_OFFSET + k) * stride]; }
     PS_D lds_float &stash(int k) const { return base[(LDS_STASH_OFFSET + k) * stride]; }
-    // Stack only: second cube's ground row c, field k (r.xyz, rhs[3], dinv[3])
+    // Stack: the stash in global memory ([LDS_STASH_FLOATS][stride] floats, this env's column)
+    float *gst = nullptr;
+    int64_t gst_stride = 0;
+    PS_D float &gstash(int k) const { return gst[k * gst_stride]; }
+    // Stack only: ground row c of cube c / NG, field k (r.xyz, rhs[3], dinv[3])
     PS_D lds_float &gnd(int c, int k) const { return base[(LDS_GND_OFFSET + c * LDS_GND_FLOATS + k) * stride]; }
     // Stack only: pair row c, field k (dir[3].xyz, rnA[3].xyz, rnB[3].xyz, rhs[3], dinv[3])
     PS_D lds_float &pair(int c, int k) const { return base[(LDS_PAIR_OFFSET + c * LDS_PAIR_FLOATS + k) * stride]; }
@@ -609,6 +615,7 @@ struct MJStore {
     PS_D MJStore opaque() const {
         MJStore r = *this;
         asm volatile("" : "+v"(r.base));
+        asm volatile("" : "+v"(r.gst));
         return r;
     }
 };
@@ -889,9 +896,9 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     }
     const float gmu = sc.fric * (float)PM_DEFAULT_FRICTION;
     if constexpr (NOBJ == 2) {
-        // unused LDS rows of the second cube must be all-zero no-ops
+        // unused LDS ground rows must be all-zero no-ops
 #pragma unroll
-        for (int c = 0; c < NG; c++)
+        for (int c = 0; c < 2 * NG; c++)
 #pragma unroll
             for (int k = 0; k < LDS_GND_FLOATS; k++) lds.gnd(c, k) = 0.0f;
     }
@@ -919,9 +926,9 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         g.lam[j] = 0.0f;
                         g.rhs[j] = j == 0 ? normal_rhs(dist, rel, g.dinv[0]) : -rel * g.dinv[j];
                     }
-                    if (NOBJ == 2 && b == 1) {
-                        // Stack: the second cube's read-only row data live in LDS
-                        const int at = ng[b];
+                    if (NOBJ == 2) {
+                        // Stack: the cubes' read-only ground-row data live in LDS
+                        const int at = b * NG + ng[b];
                         lds.gnd(at, 0) = g.r.x; lds.gnd(at, 1) = g.r.y; lds.gnd(at, 2) = g.r.z;
 #pragma unroll
                         for (int j = 0; j < 3; j++) {
@@ -1112,18 +1119,27 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     }
     PS_PHASE(3);
     __builtin_amdgcn_sched_barrier(0);
+    // per-substep values the solver never reads wait outside the registers:
+    // in LDS, or (Stack, whose LDS holds its ground rows) in the global stash
+    auto put = [&](int k, float v) {
+        if constexpr (NOBJ == 2) lds.gstash(k) = v;
+        else lds.stash(k) = v;
+    };
+    auto get = [&](const MJStore &S, int k) -> float {
+        if constexpr (NOBJ == 2) return S.gstash(k);
+        else return S.stash(k);
+    };
 #pragma unroll
     for (int d = 0; d < 9; d++) {
-        lds.stash(d) = q[d];
-        lds.stash(9 + d) = v1[d];
-        lds.stash(18 + d) = split_dq[d];
+        put(d, q[d]);
+        put(9 + d, v1[d]);
+        put(18 + d, split_dq[d]);
     }
     if constexpr (NOBJ > 0) {
-        lds.stash(27) = cw1[0].x; lds.stash(28) = cw1[0].y; lds.stash(29) = cw1[0].z;
-        lds.stash(30) = cv1[0].x; lds.stash(31) = cv1[0].y; lds.stash(32) = cv1[0].z;
-        lds.stash(33) = bd[0].pos.x; lds.stash(34) = bd[0].pos.y; lds.stash(35) = bd[0].pos.z;
-        lds.stash(36) = bd[0].quat.x; lds.stash(37) = bd[0].quat.y; lds.stash(38) = bd[0].quat.z;
-        lds.stash(39) = bd[0].quat.w;
+        put(27, cw1[0].x); put(28, cw1[0].y); put(29, cw1[0].z);
+        put(30, cv1[0].x); put(31, cv1[0].y); put(32, cv1[0].z);
+        put(33, bd[0].pos.x); put(34, bd[0].pos.y); put(35, bd[0].pos.z);
+        put(36, bd[0].quat.x); put(37, bd[0].quat.y); put(38, bd[0].quat.z); put(39, bd[0].quat.w);
     }
 
     // ---- projected Gauss-Seidel
@@ -1215,10 +1231,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     GroundContact &g = gc[b][c];
                     V3 gr = g.r;
                     float grhs = g.rhs[0], gdinv = g.dinv[0];
-                    if (NOBJ == 2 && b == 1) {  // Stack's second cube: row data in LDS
-                        gr = mk(L.gnd(c, 0), L.gnd(c, 1), L.gnd(c, 2));
-                        grhs = L.gnd(c, 3);
-                        gdinv = L.gnd(c, 6);
+                    if (NOBJ == 2) {  // Stack: row data in LDS
+                        const int at = b * NG + c;
+                        gr = mk(L.gnd(at, 0), L.gnd(at, 1), L.gnd(at, 2));
+                        grhs = L.gnd(at, 3);
+                        gdinv = L.gnd(at, 6);
                     }
                     V3 rn = mk(gr.y, -gr.x, 0.0f);  // r x (0,0,1); zero terms dropped below
                     float dl = grhs - gdinv * (rn.x * dw[b].x + rn.y * dw[b].y + dvl[b].z);
@@ -1296,12 +1313,13 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     GroundContact &g = gc[b][c];
                     V3 gr = g.r;
                     float grhs1 = g.rhs[1], grhs2 = g.rhs[2], gdinv1 = g.dinv[1], gdinv2 = g.dinv[2];
-                    if (NOBJ == 2 && b == 1) {  // Stack's second cube: row data in LDS
-                        gr = mk(L.gnd(c, 0), L.gnd(c, 1), L.gnd(c, 2));
-                        grhs1 = L.gnd(c, 4);
-                        grhs2 = L.gnd(c, 5);
-                        gdinv1 = L.gnd(c, 7);
-                        gdinv2 = L.gnd(c, 8);
+                    if (NOBJ == 2) {  // Stack: row data in LDS
+                        const int at = b * NG + c;
+                        gr = mk(L.gnd(at, 0), L.gnd(at, 1), L.gnd(at, 2));
+                        grhs1 = L.gnd(at, 4);
+                        grhs2 = L.gnd(at, 5);
+                        gdinv1 = L.gnd(at, 7);
+                        gdinv2 = L.gnd(at, 8);
                     }
                     V3 r1 = mk(gr.z, 0.0f, -gr.x);  // r x (0,-1,0)
                     V3 r2 = mk(0.0f, gr.z, -gr.y);  // r x (1,0,0)
@@ -1478,15 +1496,15 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         MJStore S = lds.opaque();
 #pragma unroll
         for (int d = 0; d < 9; d++) {
-            q[d] = S.stash(d);
-            v1[d] = S.stash(9 + d);
-            split_dq[d] = S.stash(18 + d);
+            q[d] = get(S, d);
+            v1[d] = get(S, 9 + d);
+            split_dq[d] = get(S, 18 + d);
         }
         if constexpr (NOBJ > 0) {
-            cw1[0] = mk(S.stash(27), S.stash(28), S.stash(29));
-            cv1[0] = mk(S.stash(30), S.stash(31), S.stash(32));
-            bd[0].pos = mk(S.stash(33), S.stash(34), S.stash(35));
-            bd[0].quat = Q4{S.stash(36), S.stash(37), S.stash(38), S.stash(39)};
+            cw1[0] = mk(get(S, 27), get(S, 28), get(S, 29));
+            cv1[0] = mk(get(S, 30), get(S, 31), get(S, 32));
+            bd[0].pos = mk(get(S, 33), get(S, 34), get(S, 35));
+            bd[0].quat = Q4{get(S, 36), get(S, 37), get(S, 38), get(S, 39)};
         }
     }
     // ---- integrate (btMultiBody::stepPositionsMultiDof)
