@@ -26,7 +26,7 @@ VALU_PEAK_TFLOPS = 157.3
 
 
 def algorithmic_bytes_per_env_step(obs_dim: int, action_dim: int, goal_dim: int = 3, n_objects: int = 1) -> int:
-    """Bytes one env-step must move through HBM (DESIGN.md §Roofline):
+    """Bytes one env-step must move through HBM (DESIGN.md §4, §7):
     read q,qd (18 f32), 13 f32 per object, goal (f64), TimeLimit counter,
     action; write q,qd, 45 motor f32, objects, counter, obs, ag, dg (f32),
     reward, 2 flags, final_obs + final_ag.  PandaPush-v3: 658 B."""

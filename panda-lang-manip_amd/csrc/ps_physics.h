@@ -1,6 +1,6 @@
 // ps_physics.h — per-env (one env per lane) fp32 Panda multibody step for
 // gfx950.  Same algorithm as the PyBullet 3.2.5 subset used by
-// panda_gym/pybullet.py (restated in DESIGN.md §Physics), derived for a
+// panda_gym/pybullet.py (restated in DESIGN.md §5), derived for a
 // register-resident lane:
 //   * forward kinematics with exact URDF origin rotations (12 links)
 //   * mass matrix by composite rigid bodies in the base frame, bias forces by
@@ -284,7 +284,7 @@ PS_D void spd_inverse(float M[45]) {
 }
 
 // --------------------------------------------------------------------- IK
-// calculateInverseKinematics (restated in DESIGN.md §IK): <= 20 DLS steps
+// calculateInverseKinematics (restated in DESIGN.md §5, IK): <= 20 DLS steps
 // dq = (J^T J + 0.5 I)^-1 J^T [dp; dr], pivot-frame Jacobian, 45 deg clamp.
 template <int LINK>
 PS_D void inverse_kinematics(const float q_start[9], V3 target, Q4 orn, float q_out[9]) {

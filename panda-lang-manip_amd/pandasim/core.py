@@ -68,7 +68,7 @@ class BatchedGenerator:
 def np_random(sim, seed=None) -> Tuple[BatchedGenerator, Optional[np.ndarray]]:
     """gymnasium.utils.seeding.np_random for B envs: env i is seeded with
     seed + i (an int) or seed[i] (a sequence).  seed None keeps each env's
-    current stream (the reference draws OS entropy; DESIGN.md §Host layer)."""
+    current stream (the reference draws OS entropy)."""
     seeds = None
     if seed is not None:
         if isinstance(seed, (int, np.integer)):

@@ -1,4 +1,4 @@
-"""Multi-GPU partition of the env batch (SURVEY.md §8(e), DESIGN.md §Multi-GPU).
+"""Multi-GPU partition of the env batch (SURVEY.md §8(e), DESIGN.md §8).
 
 Envs are independent, so the path shards with no exchange per step: rank r of
 W owns the contiguous global env ids [r*B/W, (r+1)*B/W) and seeds env g with

@@ -31,7 +31,7 @@ def _ptr(t: Optional[torch.Tensor]):
 
 
 class PandaSim:
-    """B Panda scenes on one GPU (one process per GPU; see DESIGN.md §Multi-GPU)."""
+    """B Panda scenes on one GPU (one process per GPU; see DESIGN.md §8)."""
 
     def __init__(self, task: str = "reach", control_type: str = "ee", reward_type: str = "sparse", num_envs: int = 1,
                  device="cuda", n_substeps: int = 20, config: Optional[L.Config] = None):

@@ -8,7 +8,7 @@ Tolerances (fp32 kernel vs fp64 oracle; BASELINE north star: 1e-3):
     2e-4, joint velocities 5e-3, object position 5e-4;
   * IK: median 1e-5 rad, max 2e-3 rad (the 1e-4 stopping rule);
   * fused env step from identical state: positions 5e-4, velocities 2e-2
-    (velocity = 50/s x IK target error, see DESIGN.md §Parity).
+    (velocity = 50/s x IK target error, see DESIGN.md §6).
 """
 import numpy as np
 import pytest
@@ -382,7 +382,7 @@ def test_large_batch_properties(ps, task):
     o = obs["observation"]
     assert torch.isfinite(o).all()
     # a gripper strike can spin the 4 cm cube to tens of rad/s (the oracle
-    # reproduces these states: DESIGN.md §Parity); everything stays physical
+    # reproduces these states: DESIGN.md §6); everything stays physical
     assert (o.abs() < 100).all()
     for body in (("object1", "object2") if task == "stack" else ("object",)):
         assert (env.sim.get_base_position(body)[:, 2] > -0.45).all()
