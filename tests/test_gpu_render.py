@@ -76,7 +76,7 @@ def _linear(depth, proj):
         return P[2, 3] / (zn + P[2, 2])  # = -z_eye = distance along the view axis
 
 
-@pytest.mark.parametrize("task", ["reach", "push", "slide", "stack", "pick_and_place"])
+@pytest.mark.parametrize("task", ["reach", "push", "slide", "stack", "pick_and_place", "flip"])
 def test_render_depth_matches_oracle_raycaster(task):
     from pandasim.envs import PandaVecEnv
 
