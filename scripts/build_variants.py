@@ -17,6 +17,9 @@ VARIANTS = {
     "unroll_off": ["-mllvm", "-amdgpu-unroll-threshold-private=0"],
     "ilp_min": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
     "no_early_if": ["-mllvm", "-amdgpu-early-ifcvt=0"],
+    # IEEE mode off: drops the v_max x,x,x canonicalisations before min/max
+    # (68 of ~3000 instructions in the Push PGS loop); NaN handling only
+    "ieee_off": ["-fno-honor-nans", "-mno-amdgpu-ieee"],
 }
 
 
