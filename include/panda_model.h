@@ -60,6 +60,11 @@
 #define PM_MOTOR_KP 0.1
 #define PM_MOTOR_KD 1.0
 #define PM_CONTACT_UPPER 1e10
+/* btContactSolverInfo defaults: SOLVER_USE_WARMSTARTING with factor 0.85 on
+ * the normal impulses of persistent contacts (friction rows start at 0), and
+ * gContactBreakingThreshold 0.02 m for matching contacts across substeps */
+#define PM_WARMSTART_FACTOR 0.85
+#define PM_CONTACT_BREAKING_THRESHOLD 0.02
 
 /* Inverse kinematics (calculateInverseKinematics defaults) */
 #define PM_IK_MAX_ITERS 20
@@ -119,18 +124,34 @@
 #define PM_BASE_X (-0.6)
 
 /*
- * Collision proxies of the gripper (the convex meshes are not available):
- * spheres in link frames.  X(link, cx, cy, cz, radius, lateral_friction)
- * fingers: panda.py:47-48 set lateral friction 1.0; hand keeps the default 0.5.
+ * Collision proxies of the hand, fingers and link 7 (PyBullet collides the
+ * URDF's convex meshes, which are not available): spheres in link frames.
+ * X(link, cx, cy, cz, radius, lateral_friction)
+ *   fingers (links 9, 10): two pad spheres each; panda.py:47-48 set their
+ *     lateral friction to 1.0;
+ *   hand (link 8): both ends of the palm bar and its centre (the palm face
+ *     between the fingers), default friction 0.5;
+ *   link 7 (PyBullet link 6, "panda_link7"): the wrist body above the flange.
+ * Contacts are offered in this order (fingers first), PM_MAX_ROBOT_CONTACTS
+ * at most.
  */
-#define PM_NUM_SPHERES 6
+#define PM_NUM_SPHERES 8
 #define PM_SPHERE_TABLE(X)                       \
     X(9, 0.0, 0.0095, 0.0205, 0.0095, 1.0)      \
     X(9, 0.0, 0.0095, 0.0445, 0.0095, 1.0)      \
     X(10, 0.0, -0.0095, 0.0205, 0.0095, 1.0)    \
     X(10, 0.0, -0.0095, 0.0445, 0.0095, 1.0)    \
     X(8, 0.0, 0.055, 0.030, 0.030, 0.5)         \
-    X(8, 0.0, -0.055, 0.030, 0.030, 0.5)
+    X(8, 0.0, -0.055, 0.030, 0.030, 0.5)        \
+    X(8, 0.0, 0.0, 0.030, 0.030, 0.5)           \
+    X(6, 0.0, 0.0, 0.060, 0.050, 0.5)
+
+/* Spinning (torsional) friction: panda.py:49-50 gives the fingers 0.001;
+ * every other body keeps btCollisionObject's default 0.  A contact's
+ * coefficient is the product of its two bodies' values
+ * (btManifoldResult::calculateCombinedSpinningFriction), so in the registered
+ * scenes (objects at 0) no contact has a torsional friction row. */
+#define PM_FINGER_SPINNING_FRICTION 0.001
 
 /* Scene (pybullet.py:726-771, tasks/{push,pick_and_place}.py: object_size 0.04, mass 1.0) */
 #define PM_TABLE_CX (-0.3)

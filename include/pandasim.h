@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PS_ABI_VERSION 3
+#define PS_ABI_VERSION 4
 
 /* the six registered tasks (panda_gym/__init__.py:8-54) */
 enum {
@@ -90,7 +90,22 @@ enum {
     PS_F_C2QUAT = 79,  /*   orientation, */
     PS_F_C2VEL = 83,   /*   linear velocity, */
     PS_F_C2OMG = 86,   /*   angular velocity */
-    PS_NUM_FLOAT_ROWS = 89,
+    /* contact cache of the warm-started solver (Bullet's persistent contact
+     * manifolds): the previous substep's contacts per group,
+     * slot by slot, with their final normal impulses.  Id rows pack the four
+     * slots' ids as sum_k id_k * 32^k (exact in f32), id = 1 + feature, 0 =
+     * empty: ground slots 1 + support point, gripper slots 1 + sphere +
+     * 8 * (0 object 1, 1 object 2, 2 ground). */
+    PS_F_WG0 = 89,     /* 4 ground-contact normal impulses of object 1 */
+    PS_F_WG0ID = 93,   /*   their packed ids */
+    PS_F_WG1 = 94,     /* object 2 (Stack) */
+    PS_F_WG1ID = 98,
+    PS_F_WR = 99,      /* 4 gripper-contact normal impulses */
+    PS_F_WRID = 103,   /*   their packed ids */
+    PS_F_WP = 104,     /* 4 object-object (Stack) normal impulses, */
+    PS_F_WPPT = 108,   /*   their points in object 1's frame (x, y, z per slot), */
+    PS_F_WPN = 120,    /*   and how many slots are in use */
+    PS_NUM_FLOAT_ROWS = 121,
     PS_NUM_RNG_ROWS = 5
 };
 

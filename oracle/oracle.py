@@ -33,12 +33,22 @@ class Body(C.Structure):
     _fields_ = [("pos", C.c_double * 3), ("quat", C.c_double * 4), ("vel", C.c_double * 3), ("omg", C.c_double * 3)]
 
 
+class Cache(C.Structure):
+    """po_cache: the warm start's contact cache (slots per group, ids 1 + feature, 0 = empty)."""
+    _fields_ = [
+        ("ground_lam", (C.c_double * 4) * 2), ("robot_lam", C.c_double * 4), ("pair_lam", C.c_double * 4),
+        ("pair_pt", (C.c_double * 3) * 4), ("ground_id", (C.c_int32 * 4) * 2), ("robot_id", C.c_int32 * 4),
+        ("pair_n", C.c_int32), ("reserved", C.c_int32),
+    ]
+
+
 class Env(C.Structure):
     _fields_ = [
         ("q", C.c_double * 9), ("qd", C.c_double * 9),
         ("m_target", C.c_double * 9), ("m_kp", C.c_double * 9), ("m_kd", C.c_double * 9),
         ("m_vel", C.c_double * 9), ("m_maximp", C.c_double * 9),
         ("obj", Body * 2), ("goal", C.c_double * 6), ("elapsed", C.c_int64), ("rng", C.c_uint64 * 5),
+        ("cache", Cache),
     ]
 
 

@@ -270,6 +270,8 @@ void po_link_frames(const po_config *cfg, const po_env *env, double R[][9], doub
     memcpy(o, k.o, sizeof k.o);
 }
 
+int po_num_spheres(void) { return PM_NUM_SPHERES; }
+
 void po_gripper_spheres(const po_config *cfg, const po_env *env, double c[][3], double r[]) {
     model_init();
     okin k;
@@ -529,10 +531,15 @@ typedef struct {
     int normal; /* for friction rows: index of the normal row */
 } orow;
 
+/* contact cache groups (po_cache): ground of object 0 / 1, gripper, pair */
+enum { CG_GROUND0 = 0, CG_GROUND1 = 1, CG_ROBOT = 2, CG_PAIR = 3 };
+
 typedef struct {
     int bodyA; /* robot link index or BODY_OBJ(i) */
     int bodyB; /* BODY_OBJ(i) or BODY_STATIC */
     double pA[3], pB[3], n[3], dist, mu;
+    int group, id; /* cache group and feature id (po_cache); pairs: point in object 1's frame */
+    double lpt[3];
 } ocontact;
 
 /* per-substep object quantities */
@@ -785,6 +792,10 @@ static void box_box_contacts(const po_config *cfg, const po_env *env, const oobj
         }
         c->dist = p->depth;
         c->mu = cfg->object_friction * cfg->object_friction;
+        c->group = CG_PAIR;
+        c->id = 0;
+        double rel[3] = {c->pB[0] - env->obj[0].pos[0], c->pB[1] - env->obj[0].pos[1], c->pB[2] - env->obj[0].pos[2]};
+        m3_tvec(ob[0].R, rel, c->lpt);
     }
 }
 
@@ -830,6 +841,8 @@ static int gen_contacts(const po_config *cfg, const po_env *env, const okin *k, 
                 c->pB[0] = pw[0]; c->pB[1] = pw[1]; c->pB[2] = top;
                 c->dist = dist;
                 c->mu = cfg->object_friction * PM_DEFAULT_FRICTION;
+                c->group = CG_GROUND0 + i;
+                c->id = 1 + v;
             }
         }
     }
@@ -857,6 +870,8 @@ static int gen_contacts(const po_config *cfg, const po_env *env, const okin *k, 
                     }
                     c->dist = dist;
                     c->mu = SPH[s].mu * cfg->object_friction;
+                    c->group = CG_ROBOT;
+                    c->id = 1 + s + 8 * i;
                 }
             }
         for (int s = 0; s < PM_NUM_SPHERES && nr < PM_MAX_ROBOT_CONTACTS; s++) {
@@ -873,6 +888,8 @@ static int gen_contacts(const po_config *cfg, const po_env *env, const okin *k, 
                 c->pB[0] = sc[s][0]; c->pB[1] = sc[s][1]; c->pB[2] = top;
                 c->dist = dist;
                 c->mu = SPH[s].mu * PM_DEFAULT_FRICTION;
+                c->group = CG_ROBOT;
+                c->id = 1 + s + 8 * 2;
             }
         }
     }
@@ -968,12 +985,58 @@ static void finish_row(orow *r, const double Minv_r[81], const oobj *ob, int n_o
     (void)v1;
 }
 
+/* Normal impulse of the previous substep's contact matching `c`
+ * (btPersistentManifold::getCacheEntry; 0 when none): by feature id for the
+ * ground and gripper contacts, whose features are fixed points of one body,
+ * and by the nearest cached point within the breaking threshold for the
+ * object-object contacts. */
+static double cache_lookup(const po_cache *k, const ocontact *c) {
+    if (c->group == CG_PAIR) {
+        double best = PM_CONTACT_BREAKING_THRESHOLD * PM_CONTACT_BREAKING_THRESHOLD, lam = 0.0;
+        for (int s = 0; s < k->pair_n; s++) {
+            double d[3] = {k->pair_pt[s][0] - c->lpt[0], k->pair_pt[s][1] - c->lpt[1], k->pair_pt[s][2] - c->lpt[2]};
+            double d2 = v3_dot(d, d);
+            if (d2 < best) { best = d2; lam = k->pair_lam[s]; }
+        }
+        return lam;
+    }
+    const int32_t *ids = c->group == CG_ROBOT ? k->robot_id : k->ground_id[c->group];
+    const double *lam = c->group == CG_ROBOT ? k->robot_lam : k->ground_lam[c->group];
+    for (int s = 0; s < PO_CACHE_SLOTS; s++)
+        if (ids[s] == c->id) return lam[s];
+    return 0.0;
+}
+
+/* the substep's contacts and final normal impulses become the cache
+ * (btMultiBodyConstraintSolver::solveGroupCacheFriendlyFinish writes
+ * m_appliedImpulse back to the manifold points) */
+static void cache_store(po_cache *k, const ocontact *cts, int nc, const orow *normals) {
+    memset(k, 0, sizeof *k);
+    int n[4] = {0, 0, 0, 0};
+    for (int c = 0; c < nc; c++) {
+        int g = cts[c].group, s = n[g]++;
+        if (s >= PO_CACHE_SLOTS) continue;
+        if (g == CG_PAIR) {
+            k->pair_lam[s] = normals[c].lam;
+            memcpy(k->pair_pt[s], cts[c].lpt, sizeof cts[c].lpt);
+            k->pair_n = s + 1;
+        } else if (g == CG_ROBOT) {
+            k->robot_lam[s] = normals[c].lam;
+            k->robot_id[s] = cts[c].id;
+        } else {
+            k->ground_lam[g][s] = normals[c].lam;
+            k->ground_id[g][s] = cts[c].id;
+        }
+    }
+}
+
 /* One btMultiBodyDynamicsWorld::stepSimulation of 1/500 s
  * (pybullet.py:52-55 calls it 20 times per env step):
  *   1. forward dynamics velocity update qd1 = qd + h M^-1 (-bias)
  *   2. constraint rows at the current positions: joint limits, joint motors,
  *      contacts (normal + 2 friction directions)
  *   3. projected Gauss-Seidel, 50 iterations or max residual^2 <= 1e-7,
+ *      normals warm-started from the contact cache (cache_lookup),
  *      non-contact rows in alternating order, then normals, then friction
  *   4. semi-implicit integration of q and of the cube pose (exp map). */
 void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
@@ -1103,8 +1166,19 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
         }
     }
 
+    /* warm start (btMultiBodyConstraintSolver::setupMultiBodyContactConstraint
+     * with SOLVER_USE_WARMSTARTING): a contact found in the previous
+     * substep's cache starts from 0.85 x its final normal impulse, applied to
+     * the velocity change before the first iteration; friction rows start at 0 */
     double dv[ND];
     memset(dv, 0, sizeof dv);
+    for (int c = 0; c < nc; c++) {
+        double prev = cache_lookup(&env->cache, &cts[c]);
+        if (prev == 0.0) continue;
+        orow *r = &rows[normal_base + c];
+        r->lam = PM_WARMSTART_FACTOR * prev;
+        for (int d = 0; d < ND; d++) dv[d] += r->MJ[d] * r->lam;
+    }
     int it;
     for (it = 0; it < PM_SOLVER_ITERATIONS; it++) {
         double res = 0.0, x;
@@ -1124,6 +1198,7 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
         }
         if (res <= PM_SOLVER_RESIDUAL_THRESHOLD || it >= PM_SOLVER_ITERATIONS - 1) break;
     }
+    cache_store(&env->cache, cts, nc, rows + normal_base);
     if (stats) {
         stats->substeps += 1;
         stats->pgs_iterations += it + 1;
@@ -1467,17 +1542,23 @@ void po_get_obs(const po_config *cfg, const po_env *env, float *obs, float *ag, 
     for (int d = 0; d < gd; d++) dg[d] = (float)env->goal[d];
 }
 
+/* set_base_pose -> resetBasePositionAndOrientation (pybullet.py:427-439):
+ * PhysicsServerCommandProcessor's init-pose command sets the base position and
+ * orientation and, with them, zero base linear and angular velocity */
 static void place_object(po_body *b, const double pos[3], const double quat[4]) {
     memcpy(b->pos, pos, sizeof(double) * 3);
     memcpy(b->quat, quat, sizeof(double) * 4);
+    memset(b->vel, 0, sizeof b->vel);
+    memset(b->omg, 0, sizeof b->omg);
 }
 
 /* RobotTaskEnv.reset (core.py:240-250): new Generator(PCG64(SeedSequence(seed)))
  * when a seed is given; Panda.reset -> neutral joints with zero velocity
  * (panda.py:121-126); Task.reset draws the goal then the object(s) in the
  * reference's order (reach.py:47-54, push.py:69-87, pick_and_place.py:65-85,
- * slide.py:69-87, stack.py:103-116, flip.py:66-78).  Object velocities are
- * not reset (only resetBasePositionAndOrientation is called). */
+ * slide.py:69-87, stack.py:103-116, flip.py:66-78).  The objects are
+ * placed at rest, and the teleport breaks every cached contact (their points
+ * drift beyond the breaking threshold), so the contact cache is emptied. */
 void po_reset(const po_config *cfg, po_env *env, int has_seed, uint64_t seed, float *obs, float *ag, float *dg) {
     model_init();
     if (has_seed) {
@@ -1537,6 +1618,7 @@ void po_reset(const po_config *cfg, po_env *env, int has_seed, uint64_t seed, fl
         }
     }
     env->elapsed = 0;
+    memset(&env->cache, 0, sizeof env->cache);
     if (obs) po_get_obs(cfg, env, obs, ag, dg);
 }
 

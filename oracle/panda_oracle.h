@@ -56,6 +56,25 @@ typedef struct {
     double pos[3], quat[4], vel[3], omg[3]; /* quat (x,y,z,w) body->world */
 } po_body;
 
+/* Contact cache of the warm-started solver (Bullet's persistent manifolds,
+ * btPersistentManifold + btContactSolverInfo::m_warmstartingFactor): the
+ * contacts of the previous substep, slot by slot in generation order, with
+ * their final normal impulses.  Ids are 1 + the contact's feature (0 = empty):
+ * ground slots of object b: 1 + support-point index; gripper slots:
+ * 1 + sphere + 8 * (0 object 1, 1 object 2, 2 ground).  Object-object (Stack)
+ * contacts have no fixed feature: they keep the contact point in object 1's
+ * frame and are matched by distance, as btPersistentManifold::getCacheEntry. */
+#define PO_CACHE_SLOTS 4
+typedef struct {
+    double ground_lam[PO_MAX_OBJECTS][PO_CACHE_SLOTS];
+    double robot_lam[PO_CACHE_SLOTS];
+    double pair_lam[PO_CACHE_SLOTS];
+    double pair_pt[PO_CACHE_SLOTS][3];
+    int32_t ground_id[PO_MAX_OBJECTS][PO_CACHE_SLOTS];
+    int32_t robot_id[PO_CACHE_SLOTS];
+    int32_t pair_n, reserved;
+} po_cache;
+
 typedef struct {
     double q[9], qd[9];
     double m_target[9], m_kp[9], m_kd[9], m_vel[9], m_maximp[9];
@@ -63,6 +82,7 @@ typedef struct {
     double goal[PO_MAX_GOAL];
     int64_t elapsed;
     uint64_t rng[5]; /* PCG64 state hi, lo, inc hi, lo; splitmix64 state of Flip's goal stream */
+    po_cache cache;
 } po_env;
 
 typedef struct {
@@ -79,6 +99,7 @@ void po_inverse_kinematics(const po_config *cfg, const double q_start[9], int li
                            const double orn[4], double q_out[9]);
 void po_control_joints(po_env *env, int n, const int32_t *joints, const double *targets, const double *forces);
 void po_link_frames(const po_config *cfg, const po_env *env, double R[][9], double o[][3]);
+int po_num_spheres(void);
 void po_gripper_spheres(const po_config *cfg, const po_env *env, double c[][3], double r[]);
 void po_substep(const po_config *cfg, po_env *env, po_stats *stats);
 void po_sim_step(const po_config *cfg, po_env *env, po_stats *stats);

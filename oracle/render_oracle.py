@@ -136,11 +136,12 @@ def scene_primitives(cfg, env):
     caps.append((on[7], on[8] + Rn[8] @ np.array(WRIST), 0.045))
     ha, hb, hr = HAND_BAR
     caps.append((on[8] + Rn[8] @ np.array(ha), on[8] + Rn[8] @ np.array(hb), hr))
-    c = (C.c_double * 3 * 6)()
-    rr = (C.c_double * 6)()
+    ns = O.lib().po_num_spheres()
+    c = (C.c_double * 3 * ns)()
+    rr = (C.c_double * ns)()
     O.lib().po_gripper_spheres.argtypes = [C.POINTER(O.Config), C.POINTER(O.Env), C.c_void_p, C.c_void_p]
     O.lib().po_gripper_spheres(C.byref(cfg), C.byref(env), c, rr)
-    sph = [(np.array([c[s][k] for k in range(3)]), rr[s]) for s in range(6)]
+    sph = [(np.array([c[s][k] for k in range(3)]), rr[s]) for s in range(ns)]
     return caps, sph
 
 

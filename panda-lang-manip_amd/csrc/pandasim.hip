@@ -173,6 +173,8 @@ PS_D void run_substeps(const KParams &P, int64_t i, int n, float q[9], float qd[
     for (int st = 0; st < n; st++) {
         int64_t ii = i;
         asm volatile("" : "+v"(ii));
+        static_assert(kBlock == 64, "WarmCache: one wave per workgroup");
+        const WarmCache wc{P.s.f + PS_F_WG0 * P.s.stride, P.s.stride};
         Motors m;
         if constexpr (STD_MOTORS) {
 #pragma unroll
@@ -180,7 +182,7 @@ PS_D void run_substeps(const KParams &P, int64_t i, int n, float q[9], float qd[
         } else {
             load_motors(P.s, ii, m);
         }
-        substep<NOBJ, SHAPE, STD_MOTORS>(P.sc, q, qd, m, bd, lds PS_PROF_ARG);
+        substep<NOBJ, SHAPE, STD_MOTORS>(P.sc, q, qd, m, bd, lds, wc PS_PROF_ARG);
     }
 }
 
@@ -332,10 +334,21 @@ PS_D void random_rotation(uint64_t &st, double q[4]) {
     q[3] = __dmul_rn(x4, t);
 }
 
+// set_base_pose -> resetBasePositionAndOrientation (pybullet.py:427-439):
+// PyBullet's init-pose command sets the base pose and, with it, zero base
+// linear and angular velocity
 PS_D void place(Body &b, double x, double y, double z) {
     b.pos = mk((float)x, (float)y, (float)z);
     b.quat = Q4{0.0f, 0.0f, 0.0f, 1.0f};
-    // the velocity is not reset (resetBasePositionAndOrientation only)
+    b.vel = mk(0.0f, 0.0f, 0.0f);
+    b.omg = mk(0.0f, 0.0f, 0.0f);
+}
+
+// a reset teleports the robot and the objects: every cached contact breaks
+// (its points drift beyond the breaking threshold)
+PS_D void clear_contact_cache(const StateView &s, int64_t i) {
+#pragma unroll
+    for (int r = PS_F_WG0; r < PS_NUM_FLOAT_ROWS; r++) s.F(r, i) = 0.0f;
 }
 
 // Panda.reset + Task.reset (core.py:245-247): goal then object draws in the
@@ -462,6 +475,7 @@ __global__ __launch_bounds__(kBlock) void k_reset(KParams P, const uint8_t *mask
     store_rng(s, i, r);
     aux_rng(s, i) = aux;
     s.elapsed[i] = 0;
+    clear_contact_cache(s, i);
     write_obs<TASK>(P, i, q, qd, bd, g, obs, ag, dg);
 }
 
@@ -517,6 +531,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
         store_rng(s, i, r);
         aux_rng(s, i) = aux;
         for (int d = 0; d < T::GOAL; d++) s.G(d, i) = g[d];
+        clear_contact_cache(s, i);
         el = 0;
     } else if (final_obs || final_ag) {
         write_obs<TASK>(P, i, q, qd, bd, g, final_obs, final_ag, nullptr);

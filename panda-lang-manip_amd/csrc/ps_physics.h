@@ -575,6 +575,7 @@ constexpr int lds_floats() { return NOBJ == 2 ? LDS_FLOATS_STACK : LDS_FLOATS; }
 struct GroundContact {
     V3 r;  // contact point - object COM
     float rhs[3], lam[3], dinv[3];
+    int id;  // contact cache id: 1 + support point (0: no contact)
 };
 
 // object-object contact (Stack): A = incident body (+n), B = reference (-n)
@@ -751,9 +752,36 @@ PS_D int box_box(const Scene &sc, const Body &b0, const Body &b1, const M3 &R0, 
 // One btMultiBodyDynamicsWorld::stepSimulation(1/500 s): see the oracle's
 // po_substep for the row-by-row restatement this mirrors.
 // PGS residual of a row is dl / dinv (the impulse change in velocity units).
-// v_rcp_f32 replaces the IEEE division; a zero dinv gives 0 * inf = NaN, which
-// fmaxf() in the residual max ignores, matching the reference's skip.
-PS_D float res_scale(float dinv) { return __builtin_amdgcn_rcpf(dinv); }
+// v_rcp_f32 replaces the IEEE division.  A lane without the row has dinv = 0
+// and dl = 0: dinv is clamped to FLT_MIN so that the residual is 0 * 2^126 = 0
+// there (the reference skips such rows), never 0 * inf = NaN -- a NaN in the
+// residual max would depend on fmaxf's NaN rule, which a build that assumes
+// no NaNs is free to change.
+PS_D float res_scale(float dinv) { return __builtin_amdgcn_rcpf(fmaxf(dinv, 1.17549435e-38f)); }
+
+// The warm start's contact cache (state rows PS_F_WG0.. of this env, see
+// include/pandasim.h): read at contact generation, written after the solve.
+// Addresses are re-derived at each access from wave-uniform values (row base,
+// stride, the wave's first env) and the lane id (v_mbcnt), so no per-lane
+// pointer or index stays live through the solve; the step kernels run one
+// 64-lane wave per workgroup, so env = blockIdx.x * 64 + lane.
+struct WarmCache {
+    float *base;  // &f[PS_F_WG0 * stride]
+    int64_t stride;
+    PS_D float &at(int row) const {
+        int64_t e = (int64_t)blockIdx.x * 64 + (int)__lane_id();
+        return base[(int64_t)(row - PS_F_WG0) * stride + e];
+    }
+};
+// slot k's id (1 + feature, 0 = empty) of a packed id row
+PS_D unsigned cache_id(unsigned pack, int k) { return (pack >> (5 * k)) & 31u; }
+// normal impulse cached for `id` among the 4 slots (0 when absent)
+PS_D float cache_lookup(const float lam[4], unsigned pack, unsigned id) {
+    float l = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; k++) l = cache_id(pack, k) == id ? lam[k] : l;
+    return l;
+}
 
 // Friction-cone projection factor (resolveConeFrictionConstraintRows): lim/|f|
 // when |f|^2 = m2 exceeds lim^2, else 1.  Raw v_rsq_f32: rsqrtf's denormal
@@ -767,8 +795,8 @@ PS_D float cone_scale(float m2, float lim) {
 // on all nine joints with the fixed Panda gains and forces, panda.py:40-56), so
 // only the targets are per-env; otherwise every gain comes from `mt`.
 template <int NOBJ, int SHAPE, bool STD_MOTORS>
-PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Body *bd, const MJStore &lds
-                  PS_PROF_PARAM) {
+PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Body *bd, const MJStore &lds,
+                  const WarmCache &wc PS_PROF_PARAM) {
     static_assert(NOBJ >= 0 && NOBJ <= 2, "objects");
     static_assert(NOBJ < 2 || SHAPE == SHAPE_BOX, "Stack stacks cubes");
     constexpr int NB = NOBJ > 0 ? NOBJ : 1;  // array extents
@@ -892,7 +920,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         ng[b] = 0;
 #pragma unroll
         for (int s = 0; s < NG; s++)
-            gc[b][s] = GroundContact{mk(0, 0, 0), {0, 0, 0}, {0, 0, 0}, {0, 0, 0}};
+            gc[b][s] = GroundContact{mk(0, 0, 0), {0, 0, 0}, {0, 0, 0}, {0, 0, 0}, 0};
     }
     const float gmu = sc.fric * (float)PM_DEFAULT_FRICTION;
     if constexpr (NOBJ == 2) {
@@ -902,8 +930,16 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
 #pragma unroll
             for (int k = 0; k < LDS_GND_FLOATS; k++) lds.gnd(c, k) = 0.0f;
     }
+    const float warm = (float)PM_WARMSTART_FACTOR;
 #pragma unroll
     for (int b = 0; b < NOBJ; b++) {
+        // the previous substep's ground contacts of this object (ids = 1 +
+        // support point, packed 5 bits per slot)
+        const int grow = b == 0 ? PS_F_WG0 : PS_F_WG1;
+        float plam[NG];
+#pragma unroll
+        for (int k = 0; k < NG; k++) plam[k] = wc.at(grow + k);
+        const unsigned pid = (unsigned)wc.at(grow + NG);
         static_for<0, num_support<SHAPE>()>([&](auto VV) {
             constexpr int V = decltype(VV)::value;
             V3 pw = bd[b].pos + mul(od[b].R, support_point<SHAPE, V>(sc));
@@ -926,6 +962,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         g.lam[j] = 0.0f;
                         g.rhs[j] = j == 0 ? normal_rhs(dist, rel, g.dinv[0]) : -rel * g.dinv[j];
                     }
+                    g.lam[0] = warm * cache_lookup(plam, pid, V + 1);
+                    g.id = V + 1;
                     if (NOBJ == 2) {
                         // Stack: the cubes' read-only ground-row data live in LDS
                         const int at = b * NG + ng[b];
@@ -935,6 +973,12 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                             lds.gnd(at, 3 + j) = g.rhs[j];
                             lds.gnd(at, 6 + j) = g.dinv[j];
                         }
+#pragma unroll
+                        for (int s = 0; s < NG; s++)
+                            if (s == ng[b]) {
+                                gc[b][s].lam[0] = g.lam[0];
+                                gc[b][s].id = g.id;
+                            }
                     } else {
 #pragma unroll
                         for (int s = 0; s < NG; s++)
@@ -944,12 +988,29 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 }
             }
         });
+        // the new ids are packed from the slots after the loop (packing inside
+        // it, by a shift of 5 * ng[b], turned the select into compile-time
+        // slots into a dynamic index and gc[][] into scratch)
+        unsigned nid = 0u;
+#pragma unroll
+        for (int k = 0; k < NG; k++) nid |= (unsigned)gc[b][k].id << (5 * k);
+        wc.at(grow + NG) = (float)nid;
     }
     PairContact pc[NP];
     int np = 0;
     if constexpr (NOBJ == 2) {
         PairCand cand[NP];
         np = box_box(sc, bd[0], bd[1], od[0].R, od[1].R, cand);
+        // the previous substep's pair contacts: points in object 1's frame,
+        // matched by distance (btPersistentManifold::getCacheEntry)
+        float pl[NP];
+        V3 ppt[NP];
+        const int pn = (int)wc.at(PS_F_WPN);
+#pragma unroll
+        for (int k = 0; k < NP; k++) {
+            pl[k] = wc.at(PS_F_WP + k);
+            ppt[k] = mk(wc.at(PS_F_WPPT + 3 * k), wc.at(PS_F_WPPT + 3 * k + 1), wc.at(PS_F_WPPT + 3 * k + 2));
+        }
         const float pmu = sc.fric * sc.fric;
         (void)pmu;
 #pragma unroll
@@ -979,6 +1040,20 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     p.lam[j] = 0.0f;
                     p.rhs[j] = j == 0 ? normal_rhs(cd.dist, rel, p.dinv[0]) : -rel * p.dinv[j];
                 }
+                V3 lp = tmul(od[0].R, cd.pB - bd[0].pos);
+                float best = (float)(PM_CONTACT_BREAKING_THRESHOLD * PM_CONTACT_BREAKING_THRESHOLD), l0 = 0.0f;
+#pragma unroll
+                for (int k = 0; k < NP; k++) {
+                    V3 d = ppt[k] - lp;
+                    float d2 = dot(d, d);
+                    bool hit = k < pn && d2 < best;
+                    best = hit ? d2 : best;
+                    l0 = hit ? pl[k] : l0;
+                }
+                p.lam[0] = warm * l0;
+                wc.at(PS_F_WPPT + 3 * c) = lp.x;
+                wc.at(PS_F_WPPT + 3 * c + 1) = lp.y;
+                wc.at(PS_F_WPPT + 3 * c + 2) = lp.z;
             } else {
                 p.a0 = true;
 #pragma unroll
@@ -999,6 +1074,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 lds.pair(c, 30 + j) = p.dinv[j];
             }
         }
+        wc.at(PS_F_WPN) = (float)np;
     }
     RobotContact rc[NR];
     int nr = 0;
@@ -1012,10 +1088,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             float dist, mu;
             int link;
             int obj;  // -1: ground
+            int id;   // cache id: 1 + sphere + 8 * (object, or 2 for the ground)
         };
         Cand slot[NR];
 #pragma unroll
-        for (int s = 0; s < NR; s++) slot[s] = Cand{mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 1), 1.0f, 0.0f, 8, -1};
+        for (int s = 0; s < NR; s++) slot[s] = Cand{mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 1), 1.0f, 0.0f, 8, -1, 0};
         auto offer = [&](const Cand &c) {
 #pragma unroll
             for (int s = 0; s < NR; s++)
@@ -1034,7 +1111,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 if (nr < NR && dist < (float)PM_CONTACT_MARGIN_SPHERE) {
                     V3 n = mul(od[b].R, nl);
                     offer(Cand{geo.spw[S] - n * (float)s.r, bd[b].pos + mul(od[b].R, cl), n, dist,
-                               (float)s.mu * sc.fric, s.link, b});
+                               (float)s.mu * sc.fric, s.link, b, 1 + S + 8 * b});
                 }
             });
         }
@@ -1046,12 +1123,18 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 float dist = geo.spw[S].z - (float)s.r - top;
                 if (dist < (float)PM_CONTACT_MARGIN_SPHERE) {
                     V3 pA = geo.spw[S] - mk(0, 0, (float)s.r);
-                    offer(Cand{pA, pA, mk(0, 0, 1), dist, (float)(s.mu * PM_DEFAULT_FRICTION), s.link, -1});
+                    offer(Cand{pA, pA, mk(0, 0, 1), dist, (float)(s.mu * PM_DEFAULT_FRICTION), s.link, -1, 1 + S + 16});
                 }
             }
         });
 #endif
-        // 2) rows of each used slot: J (registers), M^-1 J^T (LDS), rhs, bounds
+        // 2) rows of each used slot: J (registers), M^-1 J^T (LDS), rhs, bounds;
+        //    the normal starts from the cached impulse of the same feature
+        float prl[NR];
+#pragma unroll
+        for (int k = 0; k < NR; k++) prl[k] = wc.at(PS_F_WR + k);
+        const unsigned prid = (unsigned)wc.at(PS_F_WRID);
+        unsigned nrid = 0u;
 #pragma unroll
         for (int sl = 0; sl < NR; sl++) {
             RobotContact &c = rc[sl];
@@ -1100,6 +1183,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     c.lam[j] = 0.0f;
                     c.rhs[j] = j == 0 ? normal_rhs(cd.dist, rel, c.dinv[0]) : -rel * c.dinv[j];
                 }
+                c.lam[0] = warm * cache_lookup(prl, prid, (unsigned)cd.id);
+                nrid |= (unsigned)cd.id << (5 * sl);
             } else {
                 // unused slot: all-zero rows (finite M^-1 J^T too) are no-ops in PGS
                 c.mu = 0.0f;
@@ -1116,6 +1201,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 }
             }
         }
+        wc.at(PS_F_WRID) = (float)nrid;
     }
     PS_PHASE(3);
     __builtin_amdgcn_sched_barrier(0);
@@ -1219,6 +1305,55 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     };
     auto obj_dw = [&](bool o1) { return NOBJ == 2 && o1 ? dw[NB - 1] : dw[0]; };
     auto obj_dv = [&](bool o1) { return NOBJ == 2 && o1 ? dvl[NB - 1] : dvl[0]; };
+
+    // ---- warm start: the normals that matched a cached contact start from
+    // 0.85 x its impulse, applied to the velocity change before the first
+    // iteration (btMultiBodyConstraintSolver::setupMultiBodyContactConstraint);
+    // lanes without a cache hit carry lam = 0, a no-op
+    {
+        MJStore W = lds.opaque();
+#pragma unroll
+        for (int b = 0; b < NOBJ; b++)
+#pragma unroll
+            for (int c = 0; c < NG; c++)
+                if (gate_ground[b] & (1u << c)) {
+                    const float l0 = gc[b][c].lam[0];
+                    V3 gr = gc[b][c].r;
+                    if (NOBJ == 2) {
+                        const int at = b * NG + c;
+                        gr = mk(W.gnd(at, 0), W.gnd(at, 1), W.gnd(at, 2));
+                    }
+                    dw[b] = dw[b] + od[b].inv_inertia(mk(gr.y * l0, -gr.x * l0, 0.0f));
+                    dvl[b].z = fmaf(l0, od[b].inv_m, dvl[b].z);
+                }
+        if constexpr (NOBJ == 2) {
+#pragma unroll
+            for (int c = 0; c < NP; c++)
+                if (gate_pair & (1u << c)) {
+                    const float l0 = pc[c].lam[0];
+                    auto pv = [&](int k) { return mk(W.pair(c, k), W.pair(c, k + 1), W.pair(c, k + 2)); };
+                    bool A1 = !pc[c].a0;
+                    float iIA = A1 ? od[NB - 1].iI : od[0].iI, iIB = A1 ? od[0].iI : od[NB - 1].iI;
+                    float imA = A1 ? od[NB - 1].inv_m : od[0].inv_m, imB = A1 ? od[0].inv_m : od[NB - 1].inv_m;
+                    obj_add(A1, pv(9) * (l0 * iIA), pv(0) * (l0 * imA));
+                    obj_add(!A1, pv(18) * (-l0 * iIB), pv(0) * (-l0 * imB));
+                }
+        }
+#pragma unroll
+        for (int c = 0; c < NR; c++)
+            if (gate_robot & (1u << c)) {
+                const RobotContact &r = rc[c];
+                const float l0 = r.lam[0];
+#pragma unroll
+                for (int a = 0; a < 9; a++) dv[a] = fmaf(W.at(c, 0, a), l0, dv[a]);
+                if constexpr (NOBJ > 0) {
+                    float im = NOBJ == 2 && r.o1 ? od[NB - 1].inv_m : od[0].inv_m;
+                    V3 ddw = ANISO ? od[0].inv_inertia(r.rn[0] * -l0)
+                                   : r.rn[0] * (-l0 * (NOBJ == 2 && r.o1 ? od[NB - 1].iI : od[0].iI));
+                    obj_add(r.o1, ddw, r.dir[0] * (-l0 * im));
+                }
+            }
+    }
 
     auto contacts = [&]() {
         // normals: ground contacts, pair contacts, then gripper contacts
@@ -1474,6 +1609,19 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         contacts();
         if (res <= kResidualAbs) break;
     }
+
+    // the contacts' final normal impulses become the cache of the next
+    // substep (solveGroupCacheFriendlyFinish writes m_appliedImpulse back)
+#pragma unroll
+    for (int b = 0; b < NOBJ; b++)
+#pragma unroll
+        for (int c = 0; c < NG; c++) wc.at((b == 0 ? PS_F_WG0 : PS_F_WG1) + c) = gc[b][c].lam[0];
+    if constexpr (NOBJ == 2) {
+#pragma unroll
+        for (int c = 0; c < NP; c++) wc.at(PS_F_WP + c) = pc[c].lam[0];
+    }
+#pragma unroll
+    for (int c = 0; c < NR; c++) wc.at(PS_F_WR + c) = rc[c].lam[0];
 
     PS_PHASE(4);
 #ifdef PS_PROFILE_PHASES

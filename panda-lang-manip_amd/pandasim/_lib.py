@@ -21,7 +21,9 @@ F_Q, F_QD, F_MTARGET, F_MKP, F_MKD, F_MVEL, F_MIMP = 0, 9, 18, 27, 36, 45, 54
 F_CPOS, F_CQUAT, F_CVEL, F_COMG = 63, 66, 70, 73
 F_C2POS, F_C2QUAT, F_C2VEL, F_C2OMG = 76, 79, 83, 86
 OBJECT_ROWS = (F_CPOS, F_C2POS)  # pos, quat (+3), vel (+7), omg (+10) of object 0 / 1
-NUM_FLOAT_ROWS = 89
+# warm-start contact cache (ground of object 0 / 1, gripper, object-object)
+F_WG0, F_WG0ID, F_WG1, F_WG1ID, F_WR, F_WRID, F_WP, F_WPPT, F_WPN = 89, 93, 94, 98, 99, 103, 104, 108, 120
+NUM_FLOAT_ROWS = 121
 NUM_RNG_ROWS = 5
 MAX_GOAL_DIM = 6
 SHAPE_BOX, SHAPE_CYLINDER = 0, 1

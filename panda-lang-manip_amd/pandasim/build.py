@@ -10,7 +10,13 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 OUT = os.path.join(HERE, "libpandasim.so")
 SOURCES = ["pandasim.hip"]
-DEPS = ["pandasim.hip", "ps_common.h", "ps_physics.h", "ps_task.h"]
+
+
+def deps() -> list:
+    """Every source the library is built from: all of csrc/ (the kernels
+    include each header there) and the two public headers."""
+    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".h")))
+
 HEADERS = [os.path.join(ROOT, "include", h) for h in ("pandasim.h", "panda_model.h")]
 
 
@@ -27,7 +33,7 @@ def needs_build(variant: str = "") -> bool:
     if not os.path.exists(out):
         return True
     t = os.path.getmtime(out)
-    return any(os.path.getmtime(p) > t for p in [os.path.join(CSRC, d) for d in DEPS] + HEADERS)
+    return any(os.path.getmtime(p) > t for p in deps() + HEADERS)
 
 
 def build(force: bool = False, verbose: bool = True, variant: str = "", extra=()) -> str:

@@ -56,6 +56,7 @@ class PandaSim:
         self._create_ctx()
         # body name -> kind ("robot", "object", "ghost"); objects -> their index
         self._bodies: Dict[str, str] = {"panda": "robot"}
+        self.finger_spinning_friction = 0.0  # panda.py:49-50 sets 0.001 (set_spinning_friction)
         self._objects: Dict[str, int] = {}
         names = {0: [], 1: ["object"], 2: ["object1", "object2"]}[self.cfg.n_objects]
         for k, name in enumerate(names):
@@ -224,8 +225,9 @@ class PandaSim:
         if ghost:
             self._add_ghost(body_name, position)
             return
-        if spinning_friction is not None:
-            raise NotImplementedError("create_box: spinning friction of objects is not modelled")
+        if spinning_friction:
+            raise NotImplementedError("create_box: torsional friction rows (non-zero object spinning friction) "
+                                      "are not modelled")
         self._add_object(body_name, L.SHAPE_BOX, [float(x) for x in half_extents], mass, lateral_friction, position)
 
     def create_cylinder(self, body_name: str, radius: float, height: float, mass: float, position, rgba_color=None,
@@ -236,8 +238,9 @@ class PandaSim:
         if ghost:
             self._add_ghost(body_name, position)
             return
-        if spinning_friction is not None:
-            raise NotImplementedError("create_cylinder: spinning friction of objects is not modelled")
+        if spinning_friction:
+            raise NotImplementedError("create_cylinder: torsional friction rows (non-zero object spinning "
+                                      "friction) are not modelled")
         self._add_object(body_name, L.SHAPE_CYLINDER, [radius, radius, height / 2], mass, lateral_friction, position)
 
     def create_sphere(self, body_name: str, radius: float, mass: float, position, rgba_color=None,
@@ -254,9 +257,21 @@ class PandaSim:
             raise NotImplementedError("set_lateral_friction: only the Panda fingers' 1.0 is compiled in")
 
     def set_spinning_friction(self, body: str, link: int, spinning_friction: float) -> None:
-        """pybullet.py:787-799."""
-        if not (self._bodies.get(body) == "robot" and int(link) in (9, 10) and spinning_friction == 0.001):
-            raise NotImplementedError("set_spinning_friction: only the Panda fingers' 0.001 is compiled in")
+        """pybullet.py:787-799.  A contact's torsional friction coefficient is the
+        product of its two bodies' spinning frictions
+        (btManifoldResult::calculateCombinedSpinningFriction); every body but
+        the fingers keeps Bullet's default 0, so the fingers' value (panda.py:49-50)
+        yields no torsional friction row in any contact of these scenes.  A
+        non-zero value on another body would create such rows, which the kernels
+        do not build: it raises."""
+        kind = self._bodies.get(body)
+        if kind == "robot" and int(link) in (9, 10):
+            self.finger_spinning_friction = float(spinning_friction)
+            return
+        if kind in ("object", "robot") and float(spinning_friction) == 0.0:
+            return
+        raise NotImplementedError("set_spinning_friction: torsional friction rows (a non-zero spinning friction "
+                                  "on a body other than the fingers) are not modelled")
 
     def _note_visual(self, body_name, rgba_color, shape, half, ghost) -> None:
         rgba = np.zeros(4) if rgba_color is None else np.asarray(rgba_color, np.float64)  # pybullet.py:536
@@ -570,20 +585,24 @@ class PandaSim:
 
     # -------------------------------------------------------------- setters
     def set_joint_angles(self, body: str, joints: Sequence[int], angles) -> None:
-        """resetJointState (pybullet.py:441-460): position set, velocity zeroed."""
+        """resetJointState (pybullet.py:441-460): position set, velocity zeroed;
+        the robot's cached contacts break (the links are teleported)."""
         angles = torch.as_tensor(angles, dtype=torch.float32, device=self.device)
         for k, j in enumerate(joints):
             d = JOINT_TO_DOF[int(j)]
             self.f[L.F_Q + d, :self.num_envs] = angles[..., k]
             self.f[L.F_QD + d, :self.num_envs] = 0.0
+        self.f[L.F_WR:L.F_WRID + 1, :self.num_envs] = 0.0
 
     def set_joint_angle(self, body: str, joint: int, angle) -> None:
         self.set_joint_angles(body, [joint], torch.as_tensor(angle, dtype=torch.float32).reshape(-1, 1)
                               if torch.as_tensor(angle).dim() else [angle])
 
     def set_base_pose(self, body: str, position, orientation) -> None:
-        """resetBasePositionAndOrientation (pybullet.py:427-439); velocity kept.
-        A 3-vector orientation is Euler angles (getQuaternionFromEuler)."""
+        """resetBasePositionAndOrientation (pybullet.py:427-439).  PyBullet's
+        init-pose command zeroes the base linear and angular velocity with the
+        pose; the object's cached contacts break (it is teleported).  A 3-vector
+        orientation is Euler angles (getQuaternionFromEuler)."""
         orientation = torch.as_tensor(orientation, dtype=torch.float64, device=self.device)
         if orientation.shape[-1] == 3:
             orientation = quaternion_from_euler(orientation)
@@ -598,6 +617,10 @@ class PandaSim:
         row = self._object_rows(body)
         self.set_rows(row, torch.as_tensor(position, device=self.device).to(torch.float32))
         self.set_rows(row + 3, orientation.to(torch.float32))
+        self.f[row + 7:row + 13, :self.num_envs] = 0.0
+        g = L.F_WG0 if self._objects[body] == 0 else L.F_WG1
+        self.f[g:g + 5, :self.num_envs] = 0.0
+        self.f[L.F_WR:L.NUM_FLOAT_ROWS, :self.num_envs] = 0.0  # gripper and object-object contacts
 
     def control_joints(self, body: str, joints: Sequence[int], target_angles, forces) -> None:
         """setJointMotorControlArray(POSITION_CONTROL) (pybullet.py:462-477)."""

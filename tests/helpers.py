@@ -5,6 +5,14 @@ import oracle as O
 
 TASK_NAMES = ["reach", "push", "pick_and_place", "slide", "stack", "flip"]
 OBJECT_ROWS = (63, 76)
+# contact-cache rows (include/pandasim.h PS_F_WG0..PS_F_WPN)
+WG_ROWS, WR_ROW, WP_ROW, WPPT_ROW, WPN_ROW = (89, 94), 99, 104, 108, 120
+
+
+def unpack_ids(x):
+    """Four 5-bit slot ids of a packed id row (sum id_k 32^k)."""
+    v = int(x)
+    return [(v >> (5 * k)) & 31 for k in range(4)]
 
 
 def oracle_config_for(sim_cfg):
@@ -51,4 +59,15 @@ def oracle_env_from(cfg, snap, i):
     for k in range(snap["rng"].shape[0]):
         env.rng[k] = int(snap["rng"][k, i])
     env.elapsed = int(snap["elapsed"][i])
+    k = env.cache
+    for b, r in enumerate(WG_ROWS):
+        for s, idv in enumerate(unpack_ids(f[r + 4])):
+            k.ground_lam[b][s], k.ground_id[b][s] = f[r + s], idv
+    for s, idv in enumerate(unpack_ids(f[WR_ROW + 4])):
+        k.robot_lam[s], k.robot_id[s] = f[WR_ROW + s], idv
+    for s in range(4):
+        k.pair_lam[s] = f[WP_ROW + s]
+        for j in range(3):
+            k.pair_pt[s][j] = f[WPPT_ROW + 3 * s + j]
+    k.pair_n = int(f[WPN_ROW])
     return env

@@ -33,13 +33,13 @@ def test_library_exports_every_header_symbol(L):
 
 
 def test_abi_version(L):
-    assert L.lib().ps_abi_version() == 3
+    assert L.lib().ps_abi_version() == 4
 
 
 def test_state_layout(L):
     lay = L.layout(1000)
     assert lay.stride == 1024
-    assert lay.goal_offset == 89 * 1024 * 4
+    assert lay.goal_offset == 121 * 1024 * 4
     assert lay.rng_offset == lay.goal_offset + 6 * 1024 * 8
     assert lay.total_bytes == lay.rng_offset + 5 * 1024 * 8 + 1024 * 4
     assert lay.goal_offset % 8 == 0 and lay.rng_offset % 8 == 0

