@@ -105,6 +105,7 @@ def lib():
         L.po_bias_forces.argtypes = [P(Config), P(D), P(D), P(D)]
         L.po_link_inertia.argtypes = [I, P(D)]
         L.po_set_link_aabb.argtypes = [I, D, D, D]
+        L.po_set_finger_noise.argtypes = [D, C.c_uint64]
         _lib = L
     return _lib
 
@@ -253,6 +254,11 @@ def bias_forces(cfg, q, qd):
     h = np.zeros(9)
     lib().po_bias_forces(C.byref(cfg), _dp(qq), _dp(vv), _dp(h))
     return h
+
+
+def set_finger_noise(amplitude: float, seed: int = 0):
+    """Test hook: per-substep finger-position noise (panda_oracle.c)."""
+    lib().po_set_finger_noise(float(amplitude), int(seed))
 
 
 def set_link_aabb(link, lx, ly, lz):

@@ -1030,6 +1030,27 @@ static void cache_store(po_cache *k, const ocontact *cts, int nc, const orow *no
     }
 }
 
+/* Test hook (never part of the restated algorithm): when set, every substep
+ * adds a pseudo-random offset of up to +-amplitude to each finger position
+ * after integration -- of the order of one fp32 ulp of the finger range, the
+ * resolution at which the fp32 path places a finger pressed against its limit
+ * by the 170 N motor (qd = v1 + dv with |v1|, |dv| ~ 3.4 m/s cancels there).
+ * The parity tests use it to find the samples whose outcome that resolution
+ * decides (finger-limit branches). */
+static double finger_noise_amp = 0.0;
+static uint64_t finger_noise_state = 0;
+void po_set_finger_noise(double amplitude, uint64_t seed) {
+    finger_noise_amp = amplitude;
+    finger_noise_state = seed;
+}
+static double finger_noise(void) {
+    uint64_t z = (finger_noise_state += 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    return finger_noise_amp * ((double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0);
+}
+
 /* One btMultiBodyDynamicsWorld::stepSimulation of 1/500 s
  * (pybullet.py:52-55 calls it 20 times per env step):
  *   1. forward dynamics velocity update qd1 = qd + h M^-1 (-bias)
@@ -1207,11 +1228,14 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
     }
 
     /* integrate (btMultiBody::stepPositionsMultiDof) */
-    if (cfg->has_robot)
+    if (cfg->has_robot) {
         for (int d = 0; d < 9; d++) {
             env->qd[d] = v1[d] + dv[d];
             env->q[d] += dt * env->qd[d] + split_dq[d];
         }
+        if (finger_noise_amp != 0.0)
+            for (int d = 7; d < 9; d++) env->q[d] += finger_noise();
+    }
     for (int i = 0; i < cfg->n_objects; i++) {
         po_body *b = &env->obj[i];
         int o = OBJ_DOF(i);

@@ -135,6 +135,8 @@ void po_mass_matrix(const po_config *cfg, const double q[9], double M[81]);
 void po_bias_forces(const po_config *cfg, const double q[9], const double qd[9], double h[9]);
 void po_link_inertia(int link, double inertia[3]);
 void po_set_link_aabb(int link, double lx, double ly, double lz);
+/* test hook: per-substep finger-position noise of +-amplitude (0 = off), not thread-safe */
+void po_set_finger_noise(double amplitude, uint64_t seed);
 
 #ifdef __cplusplus
 }
