@@ -25,14 +25,23 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_PEAK_TFLOPS = 157.3
 
 
+def contact_cache_floats(n_objects: int) -> int:
+    """Contact-cache rows a task's step reads and writes (include/pandasim.h
+    PS_F_WG0..): 4 impulses + 1 id row per object's ground contacts and for
+    the gripper contacts; Stack adds 4 impulses, 12 points and a count."""
+    return 5 * n_objects + 5 + (17 if n_objects == 2 else 0)
+
+
 def algorithmic_bytes_per_env_step(obs_dim: int, action_dim: int, goal_dim: int = 3, n_objects: int = 1) -> int:
     """Bytes one env-step must move through HBM:
-    read q,qd (18 f32), 13 f32 per object, goal (f64), TimeLimit counter,
-    action; write q,qd, 45 motor f32, objects, counter, obs, ag, dg (f32),
-    reward, 2 flags, final_obs + final_ag.  PandaPush-v3: 658 B."""
-    read = 18 * 4 + 13 * 4 * n_objects + goal_dim * 8 + 4 + action_dim * 4
-    write = (18 * 4 + 45 * 4 + 13 * 4 * n_objects + 4 + obs_dim * 4 + 2 * goal_dim * 4 + 4 + 2 + obs_dim * 4
-             + goal_dim * 4)
+    read q,qd (18 f32), 13 f32 per object, the contact cache, goal (f64),
+    TimeLimit counter, action; write q,qd, 45 motor f32, objects, the contact
+    cache, counter, obs, ag, dg (f32), reward, 2 flags, final_obs + final_ag.
+    PandaPush-v3: 738 B."""
+    cache = contact_cache_floats(n_objects) * 4
+    read = 18 * 4 + 13 * 4 * n_objects + cache + goal_dim * 8 + 4 + action_dim * 4
+    write = (18 * 4 + 45 * 4 + 13 * 4 * n_objects + cache + 4 + obs_dim * 4 + 2 * goal_dim * 4 + 4 + 2
+             + obs_dim * 4 + goal_dim * 4)
     return read + write
 
 
@@ -86,16 +95,34 @@ def cpu_baseline(task: str, seconds: float):
         return n_env * steps / dt, used, steps, dt
 
     v1, _, s1, d1 = run(1, 64, seconds / 3)
+    work = oracle_work_counts(O, cfg)
     n_env = 16 * threads
     vn, used, sn, dn = run(threads, n_env, seconds * 2 / 3)
     O.lib().po_set_threads(1)
-    return {"value": round(vn, 2), "unit": "env-steps/s", "cores": used, "kind": "port",
+    return work, {"value": round(vn, 2), "unit": "env-steps/s", "cores": used, "kind": "port",
             "value_1core": round(v1, 2), "phase_split_1core": cpu_phase_split(O, task),
             "c1_reach_dense_1env": cpu_reach_dense_1env(O),
             "cpu_model": cpu_model(),
             "sample": f"{n_env} envs x {sn} steps of {task} (ee, sparse) in {dn:.1f} s on {used} host threads "
                       f"(OpenMP over envs) + 64 envs x {s1} steps in {d1:.1f} s on 1 thread; fp64 oracle, "
                       f"PyBullet not installed on the box"}
+
+
+def oracle_work_counts(O, cfg, n_env: int = 64, steps: int = 60) -> dict:
+    """Work counters (po_stats: PGS iterations and rows per substep, contacts,
+    IK iterations) of the oracle stepping a sample of the bench workload --
+    seeds 12345 + i, U(-1, 1) actions, auto-reset -- for the FLOP roofline."""
+    import numpy as np
+
+    envs = [O.new_env(cfg) for _ in range(n_env)]
+    for i, e in enumerate(envs):
+        O.reset(cfg, e, seed=12345 + i)
+    rng = np.random.default_rng(0xC0FFEE)
+    st = O.Stats()
+    for _ in range(steps):
+        for e in envs:
+            O.step(cfg, e, rng.uniform(-1, 1, O.action_dim(cfg)).astype(np.float32), autoreset=True, stats=st)
+    return st.as_dict()
 
 
 def cpu_model() -> str:
@@ -154,6 +181,20 @@ def cpu_reach_dense_1env(O, seconds: float = 1.0):
     return {"value": round(n / (time.perf_counter() - t0), 1), "unit": "env-steps/s", "cores": 1}
 
 
+def fp32_roofline(work: dict, n_objects: int, env_steps_per_s_per_gpu: float) -> dict:
+    """Algorithmic FP32 FLOP rate of one GPU against the vector peak
+    (pandasim/roofline.py: per-primitive costs x the oracle's work counts on
+    a sample of the same workload)."""
+    from pandasim.roofline import flops_per_env_step
+
+    f = flops_per_env_step(work, n_objects)
+    achieved = f["flops_per_env_step"] * env_steps_per_s_per_gpu / 1e12
+    return dict(f, achieved_tflops=round(achieved, 3), peak_tflops=VALU_PEAK_TFLOPS,
+                frac=round(achieved / VALU_PEAK_TFLOPS, 4),
+                note="peak = packed-FMA vector peak; the kernel issues scalar v_fma_f32 (half of it), "
+                     "and the PGS runs to the wave's slowest env (the counts are each env's own)")
+
+
 def load_pmc(workload: str, key: str = "bytes_per_launch"):
     """Per-launch PMC figures of k_step for `workload` from the committed
     rocprofv3 summary (profiles/pmc_traffic.json, scripts/summarize_profiles.py)."""
@@ -190,6 +231,9 @@ def main():
     torch.cuda.set_device(dev)
     if world > 1:
         backend = os.environ.get("PANDASIM_DIST_BACKEND", "nccl")  # "nccl" is RCCL on ROCm
+        if backend == "nccl" and world > torch.cuda.device_count():
+            raise SystemExit(f"bench.py: {world} ranks but {torch.cuda.device_count()} GPUs visible; RCCL needs one "
+                             "GPU per rank (PANDASIM_DIST_BACKEND=gloo rehearses more ranks than GPUs)")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -285,7 +329,8 @@ def main():
                            "last_success_rate": round(float(ep[1][done].mean()), 4) if done.any() else None,
                            "gathered_envs": int(ep.shape[1])}
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(spec["task"], args.cpu_seconds)
+            work, out["cpu_baseline"] = cpu_baseline(spec["task"], args.cpu_seconds)
+            out["roofline"]["fp32"] = fp32_roofline(work, env.sim.cfg.n_objects, value / world)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -154,6 +154,15 @@ int ps_step(ps_ctx *ctx, void *state, const float *actions, float *obs, float *a
             uint8_t *terminated, uint8_t *truncated, int autoreset, float *final_obs, float *final_ag,
             void *stream);
 
+/* NaN/Inf guard of ps_step (no reference counterpart; SURVEY.md §5 failure
+ * detection): with flags != NULL (device [B] u8, caller-owned, must outlive
+ * the steps) every following ps_step writes flags[i] = 1 when env i's joint
+ * or object state is not finite after the step, else 0; with
+ * reset_nonfinite != 0 such an env is also reset in-kernel (its generator
+ * continues, as in auto-reset) and reported truncated, even when ps_step's
+ * autoreset is 0.  flags == NULL and reset_nonfinite == 0 turn it off. */
+int ps_set_nonfinite_guard(ps_ctx *ctx, uint8_t *flags, int reset_nonfinite);
+
 /* Engine level: PyBullet.step() (pybullet.py:52-55) with the motors already in
  * the state (n_substeps of 1/500 s). */
 int ps_sim_step(ps_ctx *ctx, void *state, int n_substeps, void *stream);

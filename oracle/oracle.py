@@ -53,7 +53,15 @@ class Env(C.Structure):
 
 
 class Stats(C.Structure):
-    _fields_ = [("substeps", C.c_int64), ("pgs_iterations", C.c_int64), ("rows", C.c_int64), ("contacts", C.c_int64)]
+    """po_stats: work counters (panda_oracle.h)."""
+    _fields_ = [(n, C.c_int64) for n in (
+        "substeps", "pgs_iterations", "rows", "contacts",
+        "motor_rows", "limit_rows", "ground_contacts", "robot_contacts", "pair_contacts",
+        "motor_visits", "limit_visits", "ground_visits", "robot_visits", "pair_visits",
+        "steps", "ik_iterations")]
+
+    def as_dict(self) -> dict:
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
 
 
 def build() -> str:

@@ -451,8 +451,16 @@ static void ge_solve(int n, double *A, double *b, double *x) {
  * least-squares step dq = (J^T J + diag(0.5))^-1 J^T [dp; dr] clamped to
  * 45 deg max component, with the orientation error from
  * deltaQ = q* x q_ee^-1 (angle kept in float as in computeIK). */
+static void inverse_kinematics(const po_config *cfg, const double q_start[9], int link, const double pos[3],
+                               const double orn[4], double q_out[9], int64_t *iterations);
+
 void po_inverse_kinematics(const po_config *cfg, const double q_start[9], int link, const double pos[3],
                            const double orn[4], double q_out[9]) {
+    inverse_kinematics(cfg, q_start, link, pos, orn, q_out, NULL);
+}
+
+static void inverse_kinematics(const po_config *cfg, const double q_start[9], int link, const double pos[3],
+                               const double orn[4], double q_out[9], int64_t *iterations) {
     model_init();
     double q[9];
     memcpy(q, q_start, sizeof q);
@@ -462,6 +470,7 @@ void po_inverse_kinematics(const po_config *cfg, const double q_start[9], int li
     double ot[4] = {orn[0] / on, orn[1] / on, orn[2] / on, orn[3] / on};
     double diff = 1e30;
     for (int it = 0; it < PM_IK_MAX_ITERS && diff > PM_IK_RESIDUAL; it++) {
+        if (iterations) (*iterations)++;
         okin k;
         fk(cfg, q, &k);
         /* btMultiBodyTreeCreator places each body frame at the joint pivot
@@ -1221,10 +1230,24 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
     }
     cache_store(&env->cache, cts, nc, rows + normal_base);
     if (stats) {
+        int64_t n_it = it + 1, n_lim = 0, n_mot = n_noncontact, nk[4] = {0, 0, 0, 0};
+        for (int j = 0; j < n_noncontact; j++) n_lim += rows[j].hi == PM_LIMIT_MAX_IMPULSE && rows[j].lo == 0.0;
+        n_mot -= n_lim;
+        for (int c = 0; c < nc; c++) nk[cts[c].group]++;
         stats->substeps += 1;
-        stats->pgs_iterations += it + 1;
+        stats->pgs_iterations += n_it;
         stats->rows += nr;
         stats->contacts += nc;
+        stats->motor_rows += n_mot;
+        stats->limit_rows += n_lim;
+        stats->ground_contacts += nk[CG_GROUND0] + nk[CG_GROUND1];
+        stats->robot_contacts += nk[CG_ROBOT];
+        stats->pair_contacts += nk[CG_PAIR];
+        stats->motor_visits += n_it * n_mot;
+        stats->limit_visits += n_it * n_lim;
+        stats->ground_visits += n_it * (nk[CG_GROUND0] + nk[CG_GROUND1]);
+        stats->robot_visits += n_it * nk[CG_ROBOT];
+        stats->pair_visits += n_it * nk[CG_PAIR];
     }
 
     /* integrate (btMultiBody::stepPositionsMultiDof) */
@@ -1647,7 +1670,7 @@ void po_reset(const po_config *cfg, po_env *env, int has_seed, uint64_t seed, fl
 }
 
 /* Panda.set_action (panda.py:52-107) */
-static void set_action(const po_config *cfg, po_env *env, const float *action) {
+static void set_action(const po_config *cfg, po_env *env, const float *action, po_stats *stats) {
     int na = po_action_dim(cfg);
     float a[8];
     for (int i = 0; i < na; i++) a[i] = action[i] < -1.0f ? -1.0f : (action[i] > 1.0f ? 1.0f : action[i]);
@@ -1660,7 +1683,7 @@ static void set_action(const po_config *cfg, po_env *env, const float *action) {
         if (tp[2] < 0.0) tp[2] = 0.0;
         static const double orn[4] = {1.0, 0.0, 0.0, 0.0};
         double qik[9];
-        po_inverse_kinematics(cfg, env->q, PM_EE_LINK, tp, orn, qik);
+        inverse_kinematics(cfg, env->q, PM_EE_LINK, tp, orn, qik, stats ? &stats->ik_iterations : NULL);
         for (int d = 0; d < 7; d++) target[d] = qik[d];
     } else {
         for (int d = 0; d < 7; d++) target[d] = env->q[d] + (double)(a[d] * 0.05f);
@@ -1678,7 +1701,8 @@ void po_step(const po_config *cfg, po_env *env, const float *action, float *obs,
              float *reward, uint8_t *terminated, uint8_t *truncated, int autoreset, float *final_obs,
              float *final_ag, po_stats *stats) {
     model_init();
-    set_action(cfg, env, action);
+    set_action(cfg, env, action, stats);
+    if (stats) stats->steps += 1;
     po_sim_step(cfg, env, stats);
     po_get_obs(cfg, env, obs, ag, dg);
     *terminated = po_is_success(cfg->task, ag, env->goal);

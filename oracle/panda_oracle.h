@@ -85,8 +85,15 @@ typedef struct {
     po_cache cache;
 } po_env;
 
+/* Work counters (bench.py's FLOP roofline): substeps, PGS
+ * iterations, rows and contacts summed over substeps; row visits = rows of a
+ * kind x the substep's PGS iterations (one visit = one row update; friction
+ * pairs count once); IK iterations per env step. */
 typedef struct {
     int64_t substeps, pgs_iterations, rows, contacts;
+    int64_t motor_rows, limit_rows, ground_contacts, robot_contacts, pair_contacts;
+    int64_t motor_visits, limit_visits, ground_visits, robot_visits, pair_visits;
+    int64_t steps, ik_iterations;
 } po_stats;
 
 void po_default_config(po_config *cfg, int task, int control, int reward);

@@ -22,6 +22,8 @@ struct ps_ctx {
     char err[256];
     float *render_prims;  // [B][RENDER_PRIM_FLOATS] scratch of ps_render, allocated on first use
     float *gstash;        // Stack: [LDS_STASH_FLOATS][stride] substep stash, allocated on first step
+    uint8_t *nonfinite;   // ps_set_nonfinite_guard: per-env flag output of ps_step (caller-owned), or NULL
+    int reset_nonfinite;  // ... and reset such envs in-kernel
 };
 
 #ifdef PS_PROFILE_PHASES
@@ -87,6 +89,8 @@ struct KParams {
     int64_t n;
     Scene sc;
     int reward_type, block_gripper, obs_dim, action_dim, autoreset;
+    uint8_t *nonfinite;  // NaN/Inf guard output (ps_set_nonfinite_guard), NULL = off
+    int reset_nonfinite;
     float *gstash;  // Stack: [LDS_STASH_FLOATS][stride] per-substep stash (ctx scratch)
 };
 
@@ -523,7 +527,26 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
     reward[i] = reward_for(P.reward_type, dist, T::THRESHOLD);
     terminated[i] = term;
     truncated[i] = trunc;
-    if (P.autoreset && (term || trunc)) {
+    // NaN/Inf guard: a non-finite joint or object state is
+    // flagged, and with reset_nonfinite the env is reset and reported truncated
+    bool reset_bad = false;
+    if (P.nonfinite || P.reset_nonfinite) {
+        bool ok = true;
+#pragma unroll
+        for (int d = 0; d < 9; d++) ok = ok && isfinite(q[d]) && isfinite(qd[d]);
+#pragma unroll
+        for (int b = 0; b < T::NOBJ; b++)
+            ok = ok && isfinite(bd[b].pos.x + bd[b].pos.y + bd[b].pos.z + bd[b].quat.x + bd[b].quat.y + bd[b].quat.z +
+                                bd[b].quat.w + bd[b].vel.x + bd[b].vel.y + bd[b].vel.z + bd[b].omg.x + bd[b].omg.y +
+                                bd[b].omg.z);
+        if (P.nonfinite) P.nonfinite[i] = !ok;
+        if (!ok && P.reset_nonfinite) {
+            trunc = true;
+            truncated[i] = 1;
+            reset_bad = true;
+        }
+    }
+    if ((P.autoreset && (term || trunc)) || reset_bad) {
         if (final_obs || final_ag) write_obs<TASK>(P, i, q, qd, bd, g, final_obs, final_ag, nullptr);
         Pcg r = load_rng(s, i);
         uint64_t aux = aux_rng(s, i);
@@ -1100,6 +1123,8 @@ KParams params_of(ps_ctx *c, void *state) {
     P.action_dim = ps_action_dim(c);
     P.autoreset = 0;
     P.gstash = c->gstash;
+    P.nonfinite = nullptr;
+    P.reset_nonfinite = 0;
     return P;
 }
 
@@ -1264,6 +1289,8 @@ int ps_step(ps_ctx *c, void *state, const float *actions, float *obs, float *ag,
     if (ensure_stash(c) != PS_OK) return fail(c, PS_ERR_HIP, "hipMalloc of the Stack stash failed");
     KParams P = params_of(c, state);
     P.autoreset = autoreset;
+    P.nonfinite = c->nonfinite;
+    P.reset_nonfinite = c->reset_nonfinite;
     dim3 g = grid_of(P.n, kBlock), b(kBlock);
     hipStream_t st = (hipStream_t)stream;
 #define PS_LAUNCH_STEP(T, C)                                                                                     \
@@ -1286,6 +1313,13 @@ int ps_step(ps_ctx *c, void *state, const float *actions, float *obs, float *ag,
 #undef PS_LAUNCH_TASK
 #undef PS_LAUNCH_STEP
     return check_launch(c);
+}
+
+int ps_set_nonfinite_guard(ps_ctx *c, uint8_t *flags, int reset_nonfinite) {
+    if (!c) return PS_ERR_ARG;
+    c->nonfinite = flags;
+    c->reset_nonfinite = reset_nonfinite ? 1 : 0;
+    return PS_OK;
 }
 
 int ps_sim_step(ps_ctx *c, void *state, int n_substeps, void *stream) {

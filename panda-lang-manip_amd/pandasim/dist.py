@@ -5,8 +5,8 @@ W owns the contiguous global env ids [r*B/W, (r+1)*B/W) and seeds env g with
 ``seed0 + g``, which makes a W-rank run identical, env for env, to a 1-rank
 run of the same global batch.  The only collective is an optional gather of
 per-env episode statistics (returns, successes) to rank 0, once per reporting
-interval: RCCL ``all_gather_into_tensor`` over xGMI on GPUs (backend "nccl"),
-``all_gather`` under gloo (CPU tests).  One process per GPU.
+interval: ``dist.gather`` to rank 0 -- RCCL over xGMI on GPUs (backend
+"nccl"), gloo in the CPU tests.  One process per GPU.
 """
 from __future__ import annotations
 
@@ -60,23 +60,31 @@ class EpisodeStats:
 
 def gather_to_rank0(local: torch.Tensor, group=None) -> Optional[torch.Tensor]:
     """Concatenate every rank's [..., B_r] tensor along the last dim (rank
-    order = global env order).  Requires equal shard sizes (the bench's weak
-    scaling case).  Returns the full tensor on rank 0, None elsewhere; on a
-    single process it returns `local`."""
+    order = global env order) on rank 0 only (``dist.gather``: RCCL
+    point-to-point into rank 0 on GPUs, gloo on the CPU).  Shards may differ
+    in size (shard_range gives the lowest ranks one more env when the global
+    batch does not divide): every rank pads to the largest shard and rank 0
+    trims.  Returns the full tensor on rank 0, None elsewhere; on a single
+    process it returns `local`."""
     if not dist.is_available() or not dist.is_initialized():
         return local
     world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
     local = local.contiguous()
-    if dist.get_backend(group) == "nccl":
-        out = torch.empty((world,) + tuple(local.shape), dtype=local.dtype, device=local.device)
-        dist.all_gather_into_tensor(out, local, group=group)
-    else:
-        parts = [torch.empty_like(local) for _ in range(world)]
-        dist.all_gather(parts, local, group=group)
-        out = torch.stack(parts)
-    if dist.get_rank(group) != 0:
+    n = local.shape[-1]
+    sizes = torch.tensor([n], dtype=torch.int64, device=local.device)
+    all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
+    dist.all_gather(all_sizes, sizes, group=group)
+    counts = [int(t.item()) for t in all_sizes]
+    n_max = max(counts)
+    if n < n_max:
+        local = torch.cat([local, local.new_zeros(local.shape[:-1] + (n_max - n,))], dim=-1)
+    dst = dist.get_global_rank(group, 0) if group is not None else 0
+    parts = [torch.empty_like(local) for _ in range(world)] if rank == 0 else None
+    dist.gather(local, parts, dst=dst, group=group)
+    if rank != 0:
         return None
-    return torch.cat(list(out.unbind(0)), dim=-1)
+    return torch.cat([p[..., :c] for p, c in zip(parts, counts)], dim=-1)
 
 
 def max_over_ranks(value: float, device, group=None) -> float:

@@ -64,6 +64,17 @@ class PandaVecEnv:
         self._trunc = torch.zeros(B, dtype=torch.uint8, device=dev)
         self._saved_goals: Dict[int, torch.Tensor] = {}
         self._has_reset = False
+        self._nonfinite: Optional[torch.Tensor] = None
+
+    def set_nonfinite_guard(self, enabled: bool = True, reset: bool = False) -> None:
+        """NaN/Inf guard of the fused step (ps_set_nonfinite_guard): step()'s
+        info["nonfinite"] flags envs whose joint or object state is not finite;
+        with reset=True they are also reset in-kernel and reported truncated."""
+        if enabled:
+            self._nonfinite = torch.zeros(self.num_envs, dtype=torch.uint8, device=self.device)
+        else:
+            self._nonfinite = None
+        self.sim._call("ps_set_nonfinite_guard", self.sim._ctx, _ptr(self._nonfinite), int(bool(enabled and reset)))
 
     # ---------------------------------------------------------------- core
     def _obs_dict(self, obs=None, ag=None, dg=None):
@@ -106,12 +117,16 @@ class PandaVecEnv:
         if not copy:
             obs = {"observation": self._obs, "achieved_goal": self._ag, "desired_goal": self._dg}
             info = {"final_observation": self._final_obs, "final_achieved_goal": self._final_ag}
+            if self._nonfinite is not None:
+                info["nonfinite"] = self._nonfinite
             return obs, self._reward, self._term, self._trunc, info
         term, trunc = self._term.bool(), self._trunc.bool()
         info = {"is_success": term.clone()}
         if self.autoreset:
             info["final_observation"] = self._final_obs.clone()
             info["final_achieved_goal"] = self._final_ag.clone()
+        if self._nonfinite is not None:
+            info["nonfinite"] = self._nonfinite.bool()
         return self._obs_dict(), self._reward.clone(), term, trunc, info
 
     # ----------------------------------------------------------- task API

@@ -123,10 +123,27 @@ def test_bench_algorithmic_bytes_and_pmc_entries():
     sys.path.insert(0, ROOT)
     import bench
 
-    assert bench.algorithmic_bytes_per_env_step(obs_dim=18, action_dim=3) == 658  # PandaPush-v3
-    assert bench.algorithmic_bytes_per_env_step(obs_dim=6, action_dim=3, n_objects=0) == 458  # PandaReach-v3
+    # + the contact cache: 10 rows read and written (ground of the cube, gripper)
+    assert bench.algorithmic_bytes_per_env_step(obs_dim=18, action_dim=3) == 738  # PandaPush-v3
+    assert bench.algorithmic_bytes_per_env_step(obs_dim=6, action_dim=3, n_objects=0) == 498  # PandaReach-v3
     traffic = bench.load_pmc("PandaPush-v3 x65536/gpu")
     assert traffic is None or traffic > 0
     valu = bench.load_pmc("PandaPush-v3 x65536/gpu", "valu_insts_per_launch")
     assert valu is None or valu > 1e8
     assert bench.load_pmc("no such workload") is None
+
+
+def test_flop_model_counts():
+    """pandasim/roofline.py: FLOPs per env step from work counters (one step of
+    one env, 20 substeps of 30 PGS iterations over 9 motor rows and 4 ground
+    contacts, 20 IK iterations)."""
+    from pandasim import roofline as R
+
+    st = dict(steps=1, substeps=20, pgs_iterations=600, rows=0, contacts=80, motor_rows=180, limit_rows=0,
+              ground_contacts=80, robot_contacts=0, pair_contacts=0, motor_visits=20 * 30 * 9, limit_visits=0,
+              ground_visits=20 * 30 * 4, robot_visits=0, pair_visits=0, ik_iterations=20)
+    f = R.flops_per_env_step(st, n_objects=1)
+    assert f["split"]["pgs"] == 20 * 30 * (9 * R.MOTOR_ROW + 4 * R.GROUND_ROW)
+    assert f["split"]["ik"] == 20 * R.IK_ITERATION
+    assert f["pgs_iterations_per_substep"] == 30.0 and f["ik_iterations_per_step"] == 20.0
+    assert f["flops_per_env_step"] == sum(f["split"].values())

@@ -84,9 +84,9 @@ def _worker(rank, world, port, global_batch, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gloo_gather_reassembles_global_batch(world):
-    B = 12 * world
+@pytest.mark.parametrize("world,B", [(2, 24), (3, 36), (3, 37), (2, 5)])
+def test_gloo_gather_reassembles_global_batch(world, B):
+    """Equal and uneven shards (37 over 3 ranks: 13, 12, 12)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -321,3 +321,39 @@ def test_1000_random_steps_with_resets(env_id):
         steps_in_episode[done] = 0
         assert torch.isfinite(obs["observation"]).all()
     assert episodes >= B * (1000 // env.max_episode_steps)
+
+
+def test_nonfinite_guard_flags_and_resets():
+    """NaN/Inf guard: a corrupted env is flagged; with
+    reset=True it restarts from a reset state and is reported truncated,
+    while every other env steps exactly as without the guard."""
+    B = 64
+    a = torch.rand(3, B, 3, device="cuda") * 2 - 1
+    ref = make_env("push", "ee", B)
+    ref.reset(seed=3)
+    env = make_env("push", "ee", B)
+    env.reset(seed=3)
+    env.set_nonfinite_guard(True, reset=False)
+    env.sim.f[0, 5] = float("nan")  # joint 0 of env 5
+    ref.sim.f[0, 5] = 0.0
+    obs, r, te, tr, info = env.step(a[0])
+    o_ref, *_ = ref.step(a[0])
+    flags = info["nonfinite"]
+    assert bool(flags[5]) and int(flags.sum()) == 1
+    keep = torch.ones(B, dtype=torch.bool, device="cuda")
+    keep[5] = False
+    assert torch.equal(obs["observation"][keep], o_ref["observation"][keep])
+    # flag + reset: env 5 restarts (finite, elapsed 0, truncated), the rest are untouched
+    env.set_nonfinite_guard(True, reset=True)
+    obs, r, te, tr, info = env.step(a[1])
+    o_ref, _, _, tr_ref, _ = ref.step(a[1])
+    assert bool(info["nonfinite"][5]) and bool(tr[5])
+    assert torch.isfinite(obs["observation"][5]).all()
+    assert int(env.sim.elapsed[5]) == 0
+    assert torch.equal(obs["observation"][keep], o_ref["observation"][keep])
+    assert torch.equal(tr[keep], tr_ref[keep])
+    obs, r, te, tr, info = env.step(a[2])
+    assert not info["nonfinite"].any() and torch.isfinite(obs["observation"]).all()
+    env.set_nonfinite_guard(False)
+    obs, r, te, tr, info = env.step(a[2])
+    assert "nonfinite" not in info

@@ -8,6 +8,7 @@
 * seed_test.py / save_and_restore_test.py behaviours.
 """
 import copy
+import os
 
 import numpy as np
 import oracle as O
@@ -281,3 +282,16 @@ def test_threaded_batch_step_matches_serial(task):
         outs.append((obs.copy(), rew.copy()))
     O.lib().po_set_threads(1)
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+def test_oracle_clean_under_asan_ubsan():
+    """the CPU restatement built with AddressSanitizer and
+    UndefinedBehaviorSanitizer (oracle/Makefile `asan`, any report fatal),
+    driven through every entry point, all tasks and both control modes."""
+    import subprocess
+
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
+    subprocess.run(["make", "-s", "-C", here, "asan"], check=True)
+    out = subprocess.run([os.path.join(here, "build", "asan_check")], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "clean" in out.stdout
