@@ -217,6 +217,7 @@ def main():
     ap.add_argument("--batch", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--lanes", type=int, default=0, help="lanes per env of the step kernel: 1, 16, 0 = auto")
     args = ap.parse_args()
 
     import torch
@@ -244,7 +245,7 @@ def main():
     from pandasim.envs import REGISTRY
 
     B = args.batch
-    env = pandasim.make(args.env_id, num_envs=B, device=dev)
+    env = pandasim.make(args.env_id, num_envs=B, device=dev, lanes_per_env=args.lanes)
     spec = REGISTRY[args.env_id]
     # rank r owns global envs [r*B, (r+1)*B), env g seeded 12345 + g
     env.reset(seed=shard_seeds(12345, world * B, world, rank).numpy().astype("uint64"))
@@ -302,10 +303,12 @@ def main():
         "data": "synthetic (seeded resets, U(-1,1) actions)",
         "config": {"workload": workload, "env_id": args.env_id, "task": spec["task"],
                    "control": spec["control_type"], "reward": spec["reward_type"], "batch_per_gpu": B,
-                   "global_batch": world * B, "substeps": 20, "parallelism": f"batch shard x{world}"},
+                   "global_batch": world * B, "substeps": 20, "parallelism": f"batch shard x{world}",
+                   "lanes_per_env": env.lanes_per_env},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": load_pmc(workload),
-                     "kernel": f"k_step<{spec['task'].upper()},{spec['control_type'].upper()}>", "kernel_ms": round(kernel_ms, 4),
+                     "kernel": f"k_step<{spec['task'].upper()},{spec['control_type'].upper()},{env.lanes_per_env}>",
+                     "kernel_ms": round(kernel_ms, 4),
                      "bytes_per_env_step": bytes_env},
     }
     # The binding limit is VALU issue, not HBM: one wave per

@@ -24,6 +24,7 @@ struct ps_ctx {
     float *gstash;        // Stack: [LDS_STASH_FLOATS][stride] substep stash, allocated on first step
     uint8_t *nonfinite;   // ps_set_nonfinite_guard: per-env flag output of ps_step (caller-owned), or NULL
     int reset_nonfinite;  // ... and reset such envs in-kernel
+    int lanes_per_env;    // ps_set_lanes_per_env: 0 auto, 1 or 16
 };
 
 #ifdef PS_PROFILE_PHASES
@@ -171,14 +172,14 @@ PS_D uint64_t &aux_rng(const StateView &s, int64_t i) { return s.rng[4 * s.strid
 // re-read from the (L2-resident) state buffer at every substep instead of
 // occupying 45 registers through the solver.  The index goes through an empty
 // asm so the loads cannot be hoisted out of the substep loop.
-template <int NOBJ, int SHAPE, bool STD_MOTORS>
+template <int NOBJ, int SHAPE, bool STD_MOTORS, int G = 1>
 PS_D void run_substeps(const KParams &P, int64_t i, int n, float q[9], float qd[9], Body *bd,
-                       const MJStore &lds PS_PROF_PARAM) {
+                       const MJStore &lds, bool live PS_PROF_PARAM) {
     for (int st = 0; st < n; st++) {
         int64_t ii = i;
         asm volatile("" : "+v"(ii));
         static_assert(kBlock == 64, "WarmCache: one wave per workgroup");
-        const WarmCache wc{P.s.f + PS_F_WG0 * P.s.stride, P.s.stride};
+        const WarmCache<G> wc{P.s.f + PS_F_WG0 * P.s.stride, P.s.stride, live};
         Motors m;
         if constexpr (STD_MOTORS) {
 #pragma unroll
@@ -186,7 +187,7 @@ PS_D void run_substeps(const KParams &P, int64_t i, int n, float q[9], float qd[
         } else {
             load_motors(P.s, ii, m);
         }
-        substep<NOBJ, SHAPE, STD_MOTORS>(P.sc, q, qd, m, bd, lds, wc PS_PROF_ARG);
+        substep<NOBJ, SHAPE, STD_MOTORS, G>(P.sc, q, qd, m, bd, lds, wc PS_PROF_ARG);
     }
 }
 
@@ -483,14 +484,22 @@ __global__ __launch_bounds__(kBlock) void k_reset(KParams P, const uint8_t *mask
     write_obs<TASK>(P, i, q, qd, bd, g, obs, ag, dg);
 }
 
-// The fused env step: one lane = one env = one full RobotTaskEnv.step().
-template <int TASK, int CONTROL>
+// The fused env step: G lanes = one env = one full RobotTaskEnv.step().
+// G = 1: one env per lane (large batches).  G = 16 (small batches, NOBJ <= 1):
+// the 16 lanes of a group run the same setup and share the solver
+// (group_pgs); lane 0 of the group writes the env's results, and the groups
+// of the last wave past the batch end compute a copy of the last env and
+// write nothing.
+template <int TASK, int CONTROL, int G = 1>
 __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions, float *obs, float *ag, float *dg,
                                                  float *reward, uint8_t *terminated, uint8_t *truncated,
                                                  float *final_obs, float *final_ag) {
     using T = TaskTraits<TASK>;
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P.n) return;
+    const int64_t gi = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+    if (G == 1 && gi >= P.n) return;
+    const bool live = gi < P.n;
+    const int64_t i = live ? gi : P.n - 1;
+    const bool writer = G == 1 || (live && (threadIdx.x % G) == 0);
     const StateView &s = P.s;
 #ifdef PS_PROFILE_PHASES
     PhaseTimer pt;
@@ -505,7 +514,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
     {
         Motors m;
         set_action<CONTROL>(P, actions + i * P.action_dim, q, m);
-        store_motors(s, i, m);
+        if (writer) store_motors(s, i, m);
     }
     PS_PHASE(6);
     __shared__ float smem[lds_floats<T::NOBJ>() * kBlock];
@@ -514,7 +523,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
         lds.gst = P.gstash + i;
         lds.gst_stride = s.stride;
     }
-    run_substeps<T::NOBJ, T::SHAPE, true>(P, i, PM_SUBSTEPS, q, qd, bd, lds PS_PROF_ARG);
+    run_substeps<T::NOBJ, T::SHAPE, true, G>(P, i, PM_SUBSTEPS, q, qd, bd, lds, live PS_PROF_ARG);
     double g[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int d = 0; d < T::GOAL; d++) g[d] = s.G(d, i);
@@ -524,9 +533,11 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
     bool term = dist < T::THRESHOLD;
     int el = s.elapsed[i] + 1;
     bool trunc = el >= T::STEPS;
-    reward[i] = reward_for(P.reward_type, dist, T::THRESHOLD);
-    terminated[i] = term;
-    truncated[i] = trunc;
+    if (writer) {
+        reward[i] = reward_for(P.reward_type, dist, T::THRESHOLD);
+        terminated[i] = term;
+        truncated[i] = trunc;
+    }
     // NaN/Inf guard: a non-finite joint or object state is
     // flagged, and with reset_nonfinite the env is reset and reported truncated
     bool reset_bad = false;
@@ -539,31 +550,35 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
             ok = ok && isfinite(bd[b].pos.x + bd[b].pos.y + bd[b].pos.z + bd[b].quat.x + bd[b].quat.y + bd[b].quat.z +
                                 bd[b].quat.w + bd[b].vel.x + bd[b].vel.y + bd[b].vel.z + bd[b].omg.x + bd[b].omg.y +
                                 bd[b].omg.z);
-        if (P.nonfinite) P.nonfinite[i] = !ok;
+        if (P.nonfinite && writer) P.nonfinite[i] = !ok;
         if (!ok && P.reset_nonfinite) {
             trunc = true;
-            truncated[i] = 1;
+            if (writer) truncated[i] = 1;
             reset_bad = true;
         }
     }
     if ((P.autoreset && (term || trunc)) || reset_bad) {
-        if (final_obs || final_ag) write_obs<TASK>(P, i, q, qd, bd, g, final_obs, final_ag, nullptr);
+        if (writer && (final_obs || final_ag)) write_obs<TASK>(P, i, q, qd, bd, g, final_obs, final_ag, nullptr);
         Pcg r = load_rng(s, i);
         uint64_t aux = aux_rng(s, i);
         reset_env<TASK>(q, qd, bd, g, r, aux);
-        store_rng(s, i, r);
-        aux_rng(s, i) = aux;
-        for (int d = 0; d < T::GOAL; d++) s.G(d, i) = g[d];
-        clear_contact_cache(s, i);
+        if (writer) {
+            store_rng(s, i, r);
+            aux_rng(s, i) = aux;
+            for (int d = 0; d < T::GOAL; d++) s.G(d, i) = g[d];
+            clear_contact_cache(s, i);
+        }
         el = 0;
-    } else if (final_obs || final_ag) {
+    } else if (writer && (final_obs || final_ag)) {
         write_obs<TASK>(P, i, q, qd, bd, g, final_obs, final_ag, nullptr);
     }
-    s.elapsed[i] = el;
-    store_robot(s, i, q, qd);
+    if (writer) {
+        s.elapsed[i] = el;
+        store_robot(s, i, q, qd);
 #pragma unroll
-    for (int b = 0; b < T::NOBJ; b++) store_body(s, i, b, bd[b]);
-    write_obs<TASK>(P, i, q, qd, bd, g, obs, ag, dg);
+        for (int b = 0; b < T::NOBJ; b++) store_body(s, i, b, bd[b]);
+        write_obs<TASK>(P, i, q, qd, bd, g, obs, ag, dg);
+    }
 #ifdef PS_PROFILE_PHASES
     PS_PHASE(7);
     if ((threadIdx.x & 63) == 0)
@@ -593,7 +608,7 @@ __global__ __launch_bounds__(kBlock) void k_sim_step(KParams P, int n_substeps) 
     pt.last = __builtin_amdgcn_s_memtime();
     for (int k = 0; k < PS_NUM_PROF_SLOTS; k++) pt.acc[k] = 0;
 #endif
-    run_substeps<NOBJ, SHAPE, false>(P, i, n_substeps, q, qd, bd, lds PS_PROF_ARG);
+    run_substeps<NOBJ, SHAPE, false>(P, i, n_substeps, q, qd, bd, lds, true PS_PROF_ARG);
     store_robot(s, i, q, qd);
 #pragma unroll
     for (int b = 0; b < NOBJ; b++) store_body(s, i, b, bd[b]);
@@ -1291,13 +1306,23 @@ int ps_step(ps_ctx *c, void *state, const float *actions, float *obs, float *ag,
     P.autoreset = autoreset;
     P.nonfinite = c->nonfinite;
     P.reset_nonfinite = c->reset_nonfinite;
-    dim3 g = grid_of(P.n, kBlock), b(kBlock);
+    const int lanes = ps_step_lanes(c);
+    dim3 g = grid_of(P.n * lanes, kBlock), b(kBlock);
     hipStream_t st = (hipStream_t)stream;
+    // groups of 16 lanes per env exist for the one-object and robot-only tasks
 #define PS_LAUNCH_STEP(T, C)                                                                                     \
     do {                                                                                                         \
-        if constexpr (PS_TASK_ON(T))                                                                             \
+        if constexpr (PS_TASK_ON(T)) {                                                                           \
+            if constexpr (T != PS_TASK_STACK) {                                                                  \
+                if (lanes == 16) {                                                                               \
+                    hipLaunchKernelGGL((k_step<T, C, 16>), g, b, 0, st, P, actions, obs, ag, dg, reward,         \
+                                       terminated, truncated, final_obs, final_ag);                              \
+                    break;                                                                                       \
+                }                                                                                                \
+            }                                                                                                    \
             hipLaunchKernelGGL((k_step<T, C>), g, b, 0, st, P, actions, obs, ag, dg, reward, terminated,        \
                                truncated, final_obs, final_ag);                                                  \
+        }                                                                                                        \
     } while (0)
 #define PS_LAUNCH_TASK(T)                                                  \
     if (c->cfg.control == PS_CONTROL_EE) PS_LAUNCH_STEP(T, PS_CONTROL_EE); \
@@ -1313,6 +1338,19 @@ int ps_step(ps_ctx *c, void *state, const float *actions, float *obs, float *ag,
 #undef PS_LAUNCH_TASK
 #undef PS_LAUNCH_STEP
     return check_launch(c);
+}
+
+int ps_set_lanes_per_env(ps_ctx *c, int lanes) {
+    if (!c || !(lanes == 0 || lanes == 1 || lanes == 16)) return PS_ERR_ARG;
+    if (lanes == 16 && c->cfg.n_objects > 1) return fail(c, PS_ERR_UNSUPPORTED, "16 lanes per env: one object at most");
+    c->lanes_per_env = lanes;
+    return PS_OK;
+}
+
+int ps_step_lanes(const ps_ctx *c) {
+    if (!c) return PS_ERR_ARG;
+    if (c->lanes_per_env) return c->lanes_per_env;
+    return c->cfg.n_objects <= 1 && c->num_envs <= PS_GROUP_AUTO_MAX_ENVS ? 16 : 1;
 }
 
 int ps_set_nonfinite_guard(ps_ctx *c, uint8_t *flags, int reset_nonfinite) {

@@ -26,6 +26,8 @@ struct PhaseTimer {
 };
 #define PS_PROF_PARAM , PhaseTimer &pt
 #define PS_PROF_ARG , pt
+#define PS_PROF_COUNT_PARAM , int &prof_it
+#define PS_PROF_COUNT_ARG , prof_it
 #define PS_PHASE(k)                                        \
     do {                                                   \
         uint64_t ps_t_now = __builtin_amdgcn_s_memtime();  \
@@ -35,6 +37,8 @@ struct PhaseTimer {
 #else
 #define PS_PROF_PARAM
 #define PS_PROF_ARG
+#define PS_PROF_COUNT_PARAM
+#define PS_PROF_COUNT_ARG
 #define PS_PHASE(k) do {} while (0)
 #endif
 
@@ -216,6 +220,31 @@ PS_HD constexpr double joint_force(int d) {
 PS_HD constexpr double neutral_q(int d) {
     const double f[PM_NUM_DOFS] = PM_NEUTRAL_Q;
     return f[d];
+}
+
+// ------------------------------------------------------- lane groups
+// Sum over a group of 16 lanes (one DPP row), the same bits in every lane of
+// the group: each step adds a value and its partner's, and a + b == b + a
+// (row_ror:8 pairs lanes i, i^8; row_half_mirror pairs j, 7-j within each
+// half row; quad_perm [1,0,3,2] and [2,3,0,1] pair i, i^1 and i, i^2).
+template <int CTRL>
+PS_D float dpp_f(float x) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+PS_D float group16_sum(float x) {
+    x += dpp_f<0x128>(x);  // row_ror:8
+    x += dpp_f<0x141>(x);  // row_half_mirror
+    x += dpp_f<0xB1>(x);   // quad_perm [1,0,3,2]
+    x += dpp_f<0x4E>(x);   // quad_perm [2,3,0,1]
+    return x;
+}
+
+// lane K of this lane's 16-lane row, in every lane of the row (DPP
+// row_newbcast, gfx90a+)
+template <int K>
+PS_D float group16_bcast(float x) {
+    static_assert(K >= 0 && K < 16, "lane of the row");
+    return dpp_f<0x150 + K>(x);
 }
 
 // compile-time loop

@@ -763,14 +763,23 @@ PS_D float res_scale(float dinv) { return __builtin_amdgcn_rcpf(fmaxf(dinv, 1.17
 // include/pandasim.h): read at contact generation, written after the solve.
 // Addresses are re-derived at each access from wave-uniform values (row base,
 // stride, the wave's first env) and the lane id (v_mbcnt), so no per-lane
-// pointer or index stays live through the solve; the step kernels run one
-// 64-lane wave per workgroup, so env = blockIdx.x * 64 + lane.
+// pointer or index stays live through the solve.  The step kernels run one
+// 64-lane wave per workgroup with G lanes per env, so env = (blockIdx.x * 64
+// + lane) / G.  With G > 1 every lane of a group computes the same values;
+// lanes of a group past the batch end (live = false) compute a copy of the
+// last env and store nothing.
+template <int G>
 struct WarmCache {
     float *base;  // &f[PS_F_WG0 * stride]
     int64_t stride;
+    bool live;
     PS_D float &at(int row) const {
-        int64_t e = (int64_t)blockIdx.x * 64 + (int)__lane_id();
+        int64_t e = ((int64_t)blockIdx.x * 64 + (int)__lane_id()) / G;
         return base[(int64_t)(row - PS_F_WG0) * stride + e];
+    }
+    PS_D float load(int row) const { return at(row); }
+    PS_D void store(int row, float v) const {
+        if (G == 1 || live) at(row) = v;
     }
 };
 // slot k's id (1 + feature, 0 = empty) of a packed id row
@@ -791,12 +800,190 @@ PS_D float cone_scale(float m2, float lim) {
     return m2 > lim * lim ? lim * __builtin_amdgcn_rsqf(fmaxf(m2, 1.17549435e-38f)) : 1.0f;
 }
 
+// Projected Gauss-Seidel with G = 16 lanes per env (the small-batch step
+// kernel): every lane of a group ran the same setup, lane e
+// owns velocity DoF e (robot DoFs 0-8, then the object's omega 9-11 and
+// v 12-14) and keeps its slice of every row's J and M^-1 J^T.  A row is then
+// one product per lane, a 16-lane sum (group16_sum: the same bits in every
+// lane, so every lane computes the same impulse), the clamp, and one FMA per
+// lane -- about 11 instructions for a row the one-lane solver spends 20-60
+// on.  Row order, gates, bounds and the stopping rule are the one-lane
+// solver's.  Returns the full velocity change in every lane of the group.
+template <int NOBJ, int SHAPE, bool STD_MOTORS, int G>
+PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, unsigned gate_lim, unsigned lim_up,
+                    unsigned lim_on, unsigned gate_gnd, unsigned gate_robot, const float dinvj[9],
+                    const float lim_rhs[9], float lim_lam[9], const float mot_rhs[9], float mot_lam[9],
+                    GroundContact gc[NG], RobotContact rc[NR], const BodyDyn<SHAPE> &od, float gmu, float dv[9],
+                    V3 &dw, V3 &dvl PS_PROF_COUNT_PARAM) {
+    static_assert(G == 16 && NOBJ <= 1, "groups of 16 lanes hold 9 robot + 6 object DoFs");
+    const int e = (int)(__lane_id() & 15u);
+    // lane e's slices: row e of M^-1 (joint rows), object-only rows, robot rows
+    float mrow[9], midg[9];
+#pragma unroll
+    for (int d = 0; d < 9; d++) {
+        float v = 0.0f;
+#pragma unroll
+        for (int k = 0; k < 9; k++) v = e == k ? Mi[sidx(k, d)] : v;
+        mrow[d] = v;
+        midg[d] = Mi[sidx(d, d)];
+    }
+    auto oslice = [&](V3 a, V3 l) {
+        float v = 0.0f;
+        v = e == 9 ? a.x : v;
+        v = e == 10 ? a.y : v;
+        v = e == 11 ? a.z : v;
+        v = e == 12 ? l.x : v;
+        v = e == 13 ? l.y : v;
+        v = e == 14 ? l.z : v;
+        return v;
+    };
+    float gJ[NG][3], gM[NG][3];
+#pragma unroll
+    for (int c = 0; c < NG; c++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) {
+            gJ[c][j] = gM[c][j] = 0.0f;
+            if constexpr (NOBJ > 0) {
+                V3 dir = j == 0 ? mk(0, 0, 1) : (j == 1 ? mk(0, -1, 0) : mk(1, 0, 0));
+                V3 rn = cross(gc[c].r, dir);
+                gJ[c][j] = oslice(rn, dir);
+                gM[c][j] = oslice(od.inv_inertia(rn), dir * od.inv_m);
+            }
+        }
+    float rJ[NR][3], rM[NR][3];
+    {
+        const MJStore W = lds.opaque();
+        const int ke = e < 9 ? e : 8;
+#pragma unroll
+        for (int c = 0; c < NR; c++)
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                float v = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 9; k++) v = e == k ? rc[c].J[j][k] : v;
+                float m = (float)W.at(c, j, ke);
+                m = e < 9 ? m : 0.0f;
+                if constexpr (NOBJ > 0) {
+                    // the object is body B: -rn, -dir
+                    V3 rn = rc[c].rn[j], dir = rc[c].dir[j];
+                    v += oslice(mk(-rn.x, -rn.y, -rn.z), mk(-dir.x, -dir.y, -dir.z));
+                    m += oslice(od.inv_inertia(mk(-rn.x, -rn.y, -rn.z)), dir * -od.inv_m);
+                }
+                rJ[c][j] = v;
+                rM[c][j] = m;
+            }
+    }
+    float dvm = 0.0f;  // this lane's velocity change
+    // warm start (see the one-lane solver)
+#pragma unroll
+    for (int c = 0; c < NG; c++)
+        if (NOBJ > 0 && (gate_gnd & (1u << c))) dvm = fmaf(gM[c][0], gc[c].lam[0], dvm);
+#pragma unroll
+    for (int c = 0; c < NR; c++)
+        if (gate_robot & (1u << c)) dvm = fmaf(rM[c][0], rc[c].lam[0], dvm);
+
+    float res = 0.0f;
+    // a joint row's J is e_d: its product is lane d's velocity change, one
+    // DPP broadcast instead of a sum
+    auto jrow = [&](auto DD, float sgn, float rhs, float &lam, float lo, float hi) {
+        constexpr int d = decltype(DD)::value;
+        float s = group16_bcast<d>(dvm);
+        float dl = rhs - dinvj[d] * (sgn * s);
+        float nl = fminf(fmaxf(lam + dl, lo), hi);
+        dl = nl - lam;
+        lam = nl;
+        dvm = fmaf(mrow[d], sgn * dl, dvm);
+        res = fmaxf(res, fabsf(dl * midg[d]));
+    };
+    auto limit_row = [&](auto DD) {
+        constexpr int d = decltype(DD)::value;
+        if (gate_lim & (1u << d)) {
+            float sgn = (lim_up >> d) & 1u ? -1.0f : 1.0f;
+            float hi = (lim_on >> d) & 1u ? (float)PM_LIMIT_MAX_IMPULSE : 0.0f;
+            jrow(DD, sgn, lim_rhs[d], lim_lam[d], 0.0f, hi);
+        }
+    };
+    auto motor_row = [&](auto DD) {
+        constexpr int d = decltype(DD)::value;
+        float imp = STD_MOTORS ? (float)(joint_force(d) * PM_TIMESTEP) : mt.imp[d];
+        jrow(DD, 1.0f, mot_rhs[d], mot_lam[d], -imp, imp);
+    };
+    // rows d = 8..0 and 0..8 with compile-time d
+    auto down = [&](auto row) { static_for<0, 9>([&](auto K) { row(std::integral_constant<int, 8 - decltype(K)::value>{}); }); };
+    auto up = [&](auto row) { static_for<0, 9>([&](auto K) { row(K); }); };
+    auto normal = [&](float Jm, float Mm, float rhs, float dinv, float &lam) {
+        float s = group16_sum(Jm * dvm);
+        float dl = rhs - dinv * s;
+        float nl = fminf(fmaxf(lam + dl, 0.0f), (float)PM_CONTACT_UPPER);
+        dl = nl - lam;
+        lam = nl;
+        dvm = fmaf(Mm, dl, dvm);
+        res = fmaxf(res, fabsf(dl * res_scale(dinv)));
+    };
+    auto cone = [&](const float J[3], const float M[3], const float rhs[3], const float dinv[3], float lam[3],
+                    float mu) {
+        float sa = group16_sum(J[1] * dvm), sb = group16_sum(J[2] * dvm);
+        float dla = rhs[1] - dinv[1] * sa, dlb = rhs[2] - dinv[2] * sb;
+        float a = lam[1] + dla, b = lam[2] + dlb;
+        float lim = mu * fmaxf(lam[0], 0.0f);
+        float sc = cone_scale(a * a + b * b, lim);
+        a *= sc;
+        b *= sc;
+        dla = a - lam[1];
+        dlb = b - lam[2];
+        lam[1] = a;
+        lam[2] = b;
+        dvm = fmaf(M[2], dlb, fmaf(M[1], dla, dvm));
+        res = fmaxf(res, fmaxf(fabsf(dla * res_scale(dinv[1])), fabsf(dlb * res_scale(dinv[2]))));
+    };
+    auto contacts = [&]() {
+#pragma unroll
+        for (int c = 0; c < NG; c++)
+            if (NOBJ > 0 && (gate_gnd & (1u << c))) normal(gJ[c][0], gM[c][0], gc[c].rhs[0], gc[c].dinv[0], gc[c].lam[0]);
+#pragma unroll
+        for (int c = 0; c < NR; c++)
+            if (gate_robot & (1u << c)) normal(rJ[c][0], rM[c][0], rc[c].rhs[0], rc[c].dinv[0], rc[c].lam[0]);
+#pragma unroll
+        for (int c = 0; c < NG; c++)
+            if (NOBJ > 0 && (gate_gnd & (1u << c))) cone(gJ[c], gM[c], gc[c].rhs, gc[c].dinv, gc[c].lam, gmu);
+#pragma unroll
+        for (int c = 0; c < NR; c++)
+            if (gate_robot & (1u << c)) cone(rJ[c], rM[c], rc[c].rhs, rc[c].dinv, rc[c].lam, rc[c].mu);
+    };
+    constexpr float kResidualAbs = 3.16227766e-4f;
+    for (int it = 0; it < PM_SOLVER_ITERATIONS; it += 2) {
+#ifdef PS_PROFILE_PHASES
+        prof_it++;
+#endif
+        res = 0.0f;
+        down(motor_row);
+        if (gate_lim != 0u) down(limit_row);
+        contacts();
+        if (res <= kResidualAbs) break;
+#ifdef PS_PROFILE_PHASES
+        prof_it++;
+#endif
+        res = 0.0f;
+        if (gate_lim != 0u) up(limit_row);
+        up(motor_row);
+        contacts();
+        if (res <= kResidualAbs) break;
+    }
+    // every lane of the group gets the whole velocity change
+#pragma unroll
+    for (int d = 0; d < 9; d++) dv[d] = __shfl(dvm, d, G);
+    if constexpr (NOBJ > 0) {
+        dw = mk(__shfl(dvm, 9, G), __shfl(dvm, 10, G), __shfl(dvm, 11, G));
+        dvl = mk(__shfl(dvm, 12, G), __shfl(dvm, 13, G), __shfl(dvm, 14, G));
+    }
+}
+
 // STD_MOTORS: the motors are the ones RobotTaskEnv.step sets (POSITION_CONTROL
 // on all nine joints with the fixed Panda gains and forces, panda.py:40-56), so
 // only the targets are per-env; otherwise every gain comes from `mt`.
-template <int NOBJ, int SHAPE, bool STD_MOTORS>
+template <int NOBJ, int SHAPE, bool STD_MOTORS, int G = 1>
 PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Body *bd, const MJStore &lds,
-                  const WarmCache &wc PS_PROF_PARAM) {
+                  const WarmCache<G> &wc PS_PROF_PARAM) {
     static_assert(NOBJ >= 0 && NOBJ <= 2, "objects");
     static_assert(NOBJ < 2 || SHAPE == SHAPE_BOX, "Stack stacks cubes");
     constexpr int NB = NOBJ > 0 ? NOBJ : 1;  // array extents
@@ -938,8 +1125,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         const int grow = b == 0 ? PS_F_WG0 : PS_F_WG1;
         float plam[NG];
 #pragma unroll
-        for (int k = 0; k < NG; k++) plam[k] = wc.at(grow + k);
-        const unsigned pid = (unsigned)wc.at(grow + NG);
+        for (int k = 0; k < NG; k++) plam[k] = wc.load(grow + k);
+        const unsigned pid = (unsigned)wc.load(grow + NG);
         static_for<0, num_support<SHAPE>()>([&](auto VV) {
             constexpr int V = decltype(VV)::value;
             V3 pw = bd[b].pos + mul(od[b].R, support_point<SHAPE, V>(sc));
@@ -994,7 +1181,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         unsigned nid = 0u;
 #pragma unroll
         for (int k = 0; k < NG; k++) nid |= (unsigned)gc[b][k].id << (5 * k);
-        wc.at(grow + NG) = (float)nid;
+        wc.store(grow + NG, (float)nid);
     }
     PairContact pc[NP];
     int np = 0;
@@ -1005,11 +1192,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         // matched by distance (btPersistentManifold::getCacheEntry)
         float pl[NP];
         V3 ppt[NP];
-        const int pn = (int)wc.at(PS_F_WPN);
+        const int pn = (int)wc.load(PS_F_WPN);
 #pragma unroll
         for (int k = 0; k < NP; k++) {
-            pl[k] = wc.at(PS_F_WP + k);
-            ppt[k] = mk(wc.at(PS_F_WPPT + 3 * k), wc.at(PS_F_WPPT + 3 * k + 1), wc.at(PS_F_WPPT + 3 * k + 2));
+            pl[k] = wc.load(PS_F_WP + k);
+            ppt[k] = mk(wc.load(PS_F_WPPT + 3 * k), wc.load(PS_F_WPPT + 3 * k + 1), wc.load(PS_F_WPPT + 3 * k + 2));
         }
         const float pmu = sc.fric * sc.fric;
         (void)pmu;
@@ -1051,9 +1238,9 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     l0 = hit ? pl[k] : l0;
                 }
                 p.lam[0] = warm * l0;
-                wc.at(PS_F_WPPT + 3 * c) = lp.x;
-                wc.at(PS_F_WPPT + 3 * c + 1) = lp.y;
-                wc.at(PS_F_WPPT + 3 * c + 2) = lp.z;
+                wc.store(PS_F_WPPT + 3 * c, lp.x);
+                wc.store(PS_F_WPPT + 3 * c + 1, lp.y);
+                wc.store(PS_F_WPPT + 3 * c + 2, lp.z);
             } else {
                 p.a0 = true;
 #pragma unroll
@@ -1074,7 +1261,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 lds.pair(c, 30 + j) = p.dinv[j];
             }
         }
-        wc.at(PS_F_WPN) = (float)np;
+        wc.store(PS_F_WPN, (float)np);
     }
     RobotContact rc[NR];
     int nr = 0;
@@ -1132,8 +1319,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         //    the normal starts from the cached impulse of the same feature
         float prl[NR];
 #pragma unroll
-        for (int k = 0; k < NR; k++) prl[k] = wc.at(PS_F_WR + k);
-        const unsigned prid = (unsigned)wc.at(PS_F_WRID);
+        for (int k = 0; k < NR; k++) prl[k] = wc.load(PS_F_WR + k);
+        const unsigned prid = (unsigned)wc.load(PS_F_WRID);
         unsigned nrid = 0u;
 #pragma unroll
         for (int sl = 0; sl < NR; sl++) {
@@ -1201,7 +1388,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 }
             }
         }
-        wc.at(PS_F_WRID) = (float)nrid;
+        wc.store(PS_F_WRID, (float)nrid);
     }
     PS_PHASE(3);
     __builtin_amdgcn_sched_barrier(0);
@@ -1263,6 +1450,17 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     const unsigned gate_pair = wave_bits([&](int c) { return c < np; }, NP);
     const unsigned gate_robot = wave_bits([&](int c) { return c < nr; }, NR);
 
+#ifdef PS_PROFILE_PHASES
+    int prof_it = 0;
+#define PS_COUNT_IT() prof_it++
+#else
+#define PS_COUNT_IT() do {} while (0)
+#endif
+    // the solver stops when max(residual^2) <= 1e-7; tracked as max |residual|
+    // (one v_max with an abs modifier per row) against sqrt(1e-7)
+    constexpr float kResidualAbs = 3.16227766e-4f;
+    static_assert(PM_SOLVER_ITERATIONS % 2 == 0, "iteration pairs");
+    if constexpr (G == 1) {
     auto joint_row = [&](int d, float sgn, float rhs, float &lam, float lo, float hi) {
         float dl = rhs - dinvj[d] * (sgn * dv[d]);
         float nl = fminf(fmaxf(lam + dl, lo), hi);
@@ -1575,16 +1773,6 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     // reverse (motors 8..0, then limits 8..0), odd ones forward (limits 0..8,
     // then motors 0..8).  The loop is unrolled by two so both orders are
     // straight-line code; each env still stops at its own residual.
-    static_assert(PM_SOLVER_ITERATIONS % 2 == 0, "iteration pairs");
-    // the solver stops when max(residual^2) <= 1e-7; tracked as max |residual|
-    // (one v_max with an abs modifier per row) against sqrt(1e-7)
-    constexpr float kResidualAbs = 3.16227766e-4f;
-#ifdef PS_PROFILE_PHASES
-    int prof_it = 0;
-#define PS_COUNT_IT() prof_it++
-#else
-#define PS_COUNT_IT() do {} while (0)
-#endif
     for (int it = 0; it < PM_SOLVER_ITERATIONS; it += 2) {
         PS_COUNT_IT();
         L = lds.opaque();
@@ -1609,19 +1797,24 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         contacts();
         if (res <= kResidualAbs) break;
     }
+    } else {
+        group_pgs<NOBJ, SHAPE, STD_MOTORS, G>(mt, Mi, lds, gate_lim, lim_up, lim_on, gate_ground[0], gate_robot,
+                                              dinvj, lim_rhs, lim_lam, mot_rhs, mot_lam, gc[0], rc, od[0], gmu,
+                                              dv, dw[0], dvl[0] PS_PROF_COUNT_ARG);
+    }
 
     // the contacts' final normal impulses become the cache of the next
     // substep (solveGroupCacheFriendlyFinish writes m_appliedImpulse back)
 #pragma unroll
     for (int b = 0; b < NOBJ; b++)
 #pragma unroll
-        for (int c = 0; c < NG; c++) wc.at((b == 0 ? PS_F_WG0 : PS_F_WG1) + c) = gc[b][c].lam[0];
+        for (int c = 0; c < NG; c++) wc.store((b == 0 ? PS_F_WG0 : PS_F_WG1) + c, gc[b][c].lam[0]);
     if constexpr (NOBJ == 2) {
 #pragma unroll
-        for (int c = 0; c < NP; c++) wc.at(PS_F_WP + c) = pc[c].lam[0];
+        for (int c = 0; c < NP; c++) wc.store(PS_F_WP + c, pc[c].lam[0]);
     }
 #pragma unroll
-    for (int c = 0; c < NR; c++) wc.at(PS_F_WR + c) = rc[c].lam[0];
+    for (int c = 0; c < NR; c++) wc.store(PS_F_WR + c, rc[c].lam[0]);
 
     PS_PHASE(4);
 #ifdef PS_PROFILE_PHASES

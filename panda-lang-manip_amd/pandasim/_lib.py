@@ -68,7 +68,7 @@ def exported_symbols():
         "ps_obs_dim", "ps_action_dim", "ps_goal_dim", "ps_max_episode_steps", "ps_init_state", "ps_reset",
         "ps_step", "ps_sim_step", "ps_link_state", "ps_inverse_kinematics", "ps_compute_reward", "ps_rng_seed",
         "ps_rng_uniform", "ps_rng_rotation", "ps_base_state", "ps_camera", "ps_render", "ps_deproject_image",
-        "ps_deproject_pixels", "ps_set_nonfinite_guard",
+        "ps_deproject_pixels", "ps_set_nonfinite_guard", "ps_set_lanes_per_env", "ps_step_lanes",
     ]
 
 
@@ -98,6 +98,8 @@ def lib():
     L.ps_step.argtypes = [V, V, V, V, V, V, V, V, V, I, V, V, V]
     L.ps_sim_step.argtypes = [V, V, I, V]
     L.ps_set_nonfinite_guard.argtypes = [V, V, I]
+    L.ps_set_lanes_per_env.argtypes = [V, I]
+    L.ps_step_lanes.argtypes = [V]
     L.ps_link_state.argtypes = [V, V, I, V, V, V, V, V]
     L.ps_inverse_kinematics.argtypes = [V, V, I, V, V, V, V]
     L.ps_compute_reward.argtypes = [I, I, V, I, V, I, V, V, I64, V]

@@ -23,7 +23,8 @@ def main():
     env_id = sys.argv[1] if len(sys.argv) > 1 else "PandaPush-v3"
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
-    env = pandasim.make(env_id, num_envs=B)
+    lanes = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+    env = pandasim.make(env_id, num_envs=B, lanes_per_env=lanes)
     env.reset(seed=12345)
     lib = L.lib()
     lib.ps_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int]
@@ -39,8 +40,8 @@ def main():
     torch.cuda.synchronize()
     assert lib.ps_debug_phase_cycles(buf, 0) == 0
     tot = sum(buf[:8])
-    waves = (B + 63) // 64
-    print(f"{env_id} B={B}: {tot / waves / steps:.0f} wave-cycles per env-step")
+    waves = (B * env.lanes_per_env + 63) // 64
+    print(f"{env_id} B={B} lanes/env={env.lanes_per_env}: {tot / waves / steps:.0f} wave-cycles per wave-step")
     for n, v in zip(NAMES, buf[:8]):
         print(f"  {n:24s} {v / tot * 100:6.2f} %   {v / waves / steps / 20:10.0f} cyc/substep-equiv")
     subs = buf[10]  # wave-substeps counted by lane 0 of each wave

@@ -43,6 +43,9 @@ def test_every_registered_id_runs(env_id):
 
 @pytest.mark.parametrize("env_id", ["PandaPush-v3", "PandaStack-v3"])
 def test_sharded_batch_matches_unsplit_batch(env_id):
+    """The bench's 8-GPU partition (65 536 envs per GPU: the one-env-per-lane
+    kernel) with 4 shards; lanes_per_env is fixed so that the shards and the
+    full batch run the same kernel."""
     import pandasim
     from pandasim.dist import shard_seeds
 
@@ -50,11 +53,11 @@ def test_sharded_batch_matches_unsplit_batch(env_id):
     g = torch.Generator(device="cuda")
     g.manual_seed(7)
     acts = torch.rand(6, B, 3 if "Push" in env_id else 4, device="cuda", generator=g) * 2 - 1
-    full = pandasim.make(env_id, num_envs=B)
+    full = pandasim.make(env_id, num_envs=B, lanes_per_env=1)
     full.reset(seed=shard_seeds(12345, B, 1, 0).numpy().astype("uint64"))
     shards = []
     for r in range(W):
-        e = pandasim.make(env_id, num_envs=B // W)
+        e = pandasim.make(env_id, num_envs=B // W, lanes_per_env=1)
         e.reset(seed=shard_seeds(12345, B, W, r).numpy().astype("uint64"))
         shards.append(e)
     for k in range(6):
@@ -63,3 +66,27 @@ def test_sharded_batch_matches_unsplit_batch(env_id):
         for key in of:
             joined = torch.cat([p[key] for p in parts])
             assert torch.equal(of[key], joined), (env_id, k, key)
+
+
+def test_group_kernel_shards_bit_identical():
+    """The 16-lane kernel is batch-size independent too: 4 shards of 24 envs
+    step bit for bit like the 96-env batch (the ragged last wave included)."""
+    import pandasim
+    from pandasim.dist import shard_seeds
+
+    B, W = 96, 4
+    g = torch.Generator(device="cuda")
+    g.manual_seed(9)
+    acts = torch.rand(5, B, 4, device="cuda", generator=g) * 2 - 1
+    full = pandasim.make("PandaPickAndPlace-v3", num_envs=B, lanes_per_env=16)
+    full.reset(seed=shard_seeds(77, B, 1, 0).numpy().astype("uint64"))
+    shards = []
+    for r in range(W):
+        e = pandasim.make("PandaPickAndPlace-v3", num_envs=B // W, lanes_per_env=16)
+        e.reset(seed=shard_seeds(77, B, W, r).numpy().astype("uint64"))
+        shards.append(e)
+    for k in range(5):
+        of, *_ = full.step(acts[k])
+        parts = [e.step(acts[k][r * (B // W):(r + 1) * (B // W)])[0] for r, e in enumerate(shards)]
+        for key in of:
+            assert torch.equal(of[key], torch.cat([p[key] for p in parts])), (k, key)

@@ -36,10 +36,15 @@ def ps():
     return pandasim
 
 
-def make_env(ps, task, control, n, reward="sparse"):
+def make_env(ps, task, control, n, reward="sparse", lanes=0):
     from pandasim.envs import PandaVecEnv
 
-    return PandaVecEnv(task, reward, control, n, "cuda")
+    return PandaVecEnv(task, reward, control, n, "cuda", lanes_per_env=lanes)
+
+
+# ps_step kernels: one env per lane, and groups of 16 lanes per env (not Stack)
+LANES = [1, 16]
+TASKS_LANES = [(t, c, l) for t, c in TASKS for l in LANES if not (t == "stack" and l == 16)]
 
 
 # ------------------------------------------------------------ known answers
@@ -331,11 +336,12 @@ def _ill_conditioned(cfg, snap, i, action, o_ref, groups, tol):
     return False
 
 
-@pytest.mark.parametrize("task,control", TASKS)
-def test_env_step_parity_teacher_forced(ps, task, control):
+@pytest.mark.parametrize("task,control,lanes", TASKS_LANES)
+def test_env_step_parity_teacher_forced(ps, task, control, lanes):
     """Each fused GPU env step vs one oracle env step from the same state."""
     B, steps = 64, 10
-    env = make_env(ps, task, control, B)
+    env = make_env(ps, task, control, B, lanes=lanes)
+    assert env.lanes_per_env == lanes
     env.autoreset = False
     env.reset(seed=12345)
     cfg = oracle_config_for(env.sim.cfg)
@@ -371,7 +377,7 @@ def test_env_step_parity_teacher_forced(ps, task, control):
                     worst[k] = max(worst[k], err_n)
             assert t_r == bool(tr[i])
             flag_mismatch += t_e != bool(te[i])
-    print(task, control, {k: f"{v:.2e}" for k, v in worst.items()},
+    print(task, control, f"lanes {lanes}", {k: f"{v:.2e}" for k, v in worst.items()},
           f"ill-conditioned (finger-limit) samples {n_bif}/{B * steps}", {k: f"{v:.2e}" for k, v in worst_bif.items()})
     for k, v in worst.items():
         assert v <= TOL[task][k], (k, v)
@@ -556,12 +562,13 @@ def test_gripper_object_contact_parity(ps, task):
     assert e_obj.max() < 2e-2 and e_q.max() < SIM_LOOSE["q"] * 5
 
 
-@pytest.mark.parametrize("B", [1, 70])
-def test_ragged_batch_parity(ps, B):
-    """Batches that are not a multiple of the 64-lane wave (one env; 70 = a
-    full wave plus a 6-lane one): every env, including the ragged wave's,
+@pytest.mark.parametrize("B,lanes", [(1, 1), (70, 1), (1, 16), (7, 16), (70, 16)])
+def test_ragged_batch_parity(ps, B, lanes):
+    """Batches that are not a multiple of the wave (one env; 70 = a full
+    64-lane wave plus 6 lanes; with 16 lanes per env, 7 envs = a wave of 4
+    plus 3 envs and a dummy group): every env, including the ragged wave's,
     steps like the oracle from the same state."""
-    env = make_env(ps, "push", "ee", B)
+    env = make_env(ps, "push", "ee", B, lanes=lanes)
     env.autoreset = False
     env.reset(seed=4242)
     cfg = oracle_config_for(env.sim.cfg)
