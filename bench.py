@@ -190,7 +190,7 @@ def fp32_roofline(work: dict, n_objects: int, env_steps_per_s_per_gpu: float) ->
     f = flops_per_env_step(work, n_objects)
     achieved = f["flops_per_env_step"] * env_steps_per_s_per_gpu / 1e12
     return dict(f, achieved_tflops=round(achieved, 3), peak_tflops=VALU_PEAK_TFLOPS,
-                frac=round(achieved / VALU_PEAK_TFLOPS, 4),
+                frac=round(achieved / VALU_PEAK_TFLOPS, 4), unit="TFLOP/s",
                 note="peak = packed-FMA vector peak; the kernel issues scalar v_fma_f32 (half of it), "
                      "and the PGS runs to the wave's slowest env (the counts are each env's own)")
 
@@ -324,6 +324,13 @@ def main():
             "peak_one_wave_per_simd": round(simds * clk / 4 / 1e9, 2), "peak_dual_issue": round(simds * clk / 2 / 1e9, 2),
             "frac_one_wave_per_simd": round(rate / (simds * clk / 4), 4),
             "valu_insts_per_launch": valu, "source": "profiles/pmc_traffic.json (SQ_INSTS_VALU)"}
+    executed = load_pmc(workload, "fp32_flops_executed_per_launch")
+    if executed:
+        rate = executed / (kernel_ms * 1e-3) / 1e12
+        out["roofline"]["fp32_executed"] = {
+            "achieved_tflops": round(rate, 3), "peak_tflops": VALU_PEAK_TFLOPS, "frac": round(rate / VALU_PEAK_TFLOPS, 4),
+            "flops_per_launch": executed,
+            "source": "profiles/pmc_traffic.json (SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32 x 64 lanes, FMA = 2)"}
     if rank == 0:
         ep = episode_stats.double().cpu()
         done = ep[2] > 0

@@ -100,6 +100,13 @@ def main():
             acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
         for k, cs in acc.items():
             extra[k] = {c: sum(v) / len(v) for c, v in cs.items()}
+    fpath = os.path.join(OUT, f"{args.prefix}_flops", "run_counter_collection.csv")
+    if os.path.exists(fpath):
+        acc = collections.defaultdict(lambda: collections.defaultdict(list))
+        for r in csv.DictReader(open(fpath)):
+            acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, cs in acc.items():
+            extra[k].update({c: sum(v) / len(v) for c, v in cs.items()})
     factor, calib = 2.0, calibrate()
     if calib and calib.get("fetch_factor"):
         factor = float(calib["fetch_factor"])
@@ -131,6 +138,12 @@ def main():
         sq = kernels[step[0]].get("sq_counters_per_launch", {})
         if "SQ_INSTS_VALU" in sq:
             traffic[args.workload]["valu_insts_per_launch"] = round(sq["SQ_INSTS_VALU"])
+        if "SQ_INSTS_VALU_FMA_F32" in sq:
+            # executed FP32 FLOPs: wave instructions x 64 lanes (FMA = 2), an upper
+            # bound when lanes are masked off (converged PGS lanes)
+            traffic[args.workload]["fp32_flops_executed_per_launch"] = round(64 * (
+                2 * sq["SQ_INSTS_VALU_FMA_F32"] + sq.get("SQ_INSTS_VALU_ADD_F32", 0) +
+                sq.get("SQ_INSTS_VALU_MUL_F32", 0) + sq.get("SQ_INSTS_VALU_TRANS_F32", 0)))
         json.dump(traffic, open(tpath, "w"), indent=1)
     for k, e in sorted(kernels.items(), key=lambda kv: -kv[1]["avg_ns_all"] * kv[1]["launches"])[:4]:
         print(k, {x: (round(v, 1) if isinstance(v, float) else v) for x, v in e.items()

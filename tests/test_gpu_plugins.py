@@ -66,7 +66,9 @@ def test_plugin_path_matches_fused_kernel(ps, task, control):
     from pandasim.envs import PandaVecEnv
 
     B = 128
-    fused = PandaVecEnv(task, "dense", control, B, "cuda", autoreset=False)
+    # the plugin path steps through ps_sim_step (one env per lane): compare it
+    # with the one-lane step kernel, the same arithmetic
+    fused = PandaVecEnv(task, "dense", control, B, "cuda", autoreset=False, lanes_per_env=1)
     fused.reset(seed=777)
     env = ps.make(f"{ENV_IDS[task]}{'Joints' if control == 'joints' else ''}Dense-v3", num_envs=B, fused=False)
     env.reset(seed=777)
