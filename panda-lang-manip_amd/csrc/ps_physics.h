@@ -554,18 +554,20 @@ constexpr int LDS_FLOATS = LDS_MI_OFFSET + 45;
 constexpr int LDS_FLOATS = LDS_MI_OFFSET;
 #endif
 // Stack (two cubes) keeps the read-only data of both cubes' ground rows (r,
-// rhs, dinv: 9 per contact) and of the box-box pair rows (dir, rA x dir,
-// rB x dir, rhs, dinv: 33 per contact) in LDS instead of registers, where they
-// spilled ~1.8 KB per lane to scratch beyond L2.  Its 40-float stash moves to a
-// global per-env buffer (written once and read once per substep, L2-resident)
-// and the ground rows take its LDS place: 312 floats per lane = 78 KB per
-// 64-lane workgroup, two workgroups per CU (two rounds of 65 536 envs).
-constexpr int LDS_GND_OFFSET = LDS_STASH_OFFSET;
+// rhs, dinv: 9 per contact) and of the box-box pair rows (dir[3], rA, rB, rhs,
+// dinv: 21 per contact; the pair rows' r x dir are rebuilt in the loop) in LDS
+// instead of registers, where they spilled ~1.8 KB per lane to scratch beyond
+// L2.  Its gripper rows' M^-1 J^T are not stored: the loop forms them from
+// M^-1 (registers) and J, and its 40-float stash moves to a global per-env
+// buffer (written once and read once per substep, L2-resident).  That is 156
+// floats per lane = 39 KB per 64-lane workgroup: four workgroups per CU, one
+// wave per SIMD, as the one-object scenes.
+constexpr int LDS_GND_OFFSET = 0;
 constexpr int LDS_GND_FLOATS = 9;
 constexpr int LDS_PAIR_OFFSET = LDS_GND_OFFSET + 2 * NG * LDS_GND_FLOATS;
-constexpr int LDS_PAIR_FLOATS = 33;
+constexpr int LDS_PAIR_FLOATS = 21;
 constexpr int LDS_FLOATS_STACK = LDS_PAIR_OFFSET + NP * LDS_PAIR_FLOATS;
-static_assert(LDS_FLOATS_STACK * 4 * 64 * 2 <= 160 * 1024, "two Stack workgroups per CU");
+static_assert(LDS_FLOATS_STACK * 4 * 64 * 4 <= 160 * 1024, "four Stack workgroups per CU");
 template <int NOBJ>
 constexpr int lds_floats() { return NOBJ == 2 ? LDS_FLOATS_STACK : LDS_FLOATS; }
 
@@ -580,7 +582,7 @@ struct GroundContact {
 
 // object-object contact (Stack): A = incident body (+n), B = reference (-n)
 struct PairContact {
-    V3 dir[3], rnA[3], rnB[3];
+    V3 dir[3], rA, rB;  // rA, rB: contact point - COM of A, B
     float rhs[3], lam[3], dinv[3];
     bool a0;  // body A is object 0
 };
@@ -608,7 +610,7 @@ struct MJStore {
     PS_D float &gstash(int k) const { return gst[k * gst_stride]; }
     // Stack only: ground row c of cube c / NG, field k (r.xyz, rhs[3], dinv[3])
     PS_D lds_float &gnd(int c, int k) const { return base[(LDS_GND_OFFSET + c * LDS_GND_FLOATS + k) * stride]; }
-    // Stack only: pair row c, field k (dir[3].xyz, rnA[3].xyz, rnB[3].xyz, rhs[3], dinv[3])
+    // Stack only: pair row c, field k (dir[3].xyz, rA.xyz, rB.xyz, rhs[3], dinv[3])
     PS_D lds_float &pair(int c, int k) const { return base[(LDS_PAIR_OFFSET + c * LDS_PAIR_FLOATS + k) * stride]; }
     // a copy whose address the compiler cannot see through: loads from it are
     // not loop-invariant, so they stay in the PGS loop as ds_reads instead of
@@ -1211,19 +1213,20 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 plane_space(cd.n, dirs[1], dirs[2]);
                 V3 rA = cd.pA - (A == 0 ? bd[0].pos : bd[1].pos), rB = cd.pB - (A == 0 ? bd[1].pos : bd[0].pos);
                 p.a0 = cd.a0;
+                p.rA = rA;
+                p.rB = rB;
 #pragma unroll
                 for (int j = 0; j < 3; j++) {
                     V3 dj = dirs[j];
                     p.dir[j] = dj;
-                    p.rnA[j] = cross(rA, dj);
-                    p.rnB[j] = cross(rB, dj);
+                    const V3 rnA = cross(rA, dj), rnB = cross(rB, dj);
                     float iIA = A == 0 ? od[0].iI : od[1].iI, iIB = A == 0 ? od[1].iI : od[0].iI;
                     float imA = A == 0 ? od[0].inv_m : od[1].inv_m, imB = A == 0 ? od[1].inv_m : od[0].inv_m;
-                    float den = dot(p.rnA[j], p.rnA[j]) * iIA + dot(p.rnB[j], p.rnB[j]) * iIB + dot(dj, dj) * (imA + imB);
+                    float den = dot(rnA, rnA) * iIA + dot(rnB, rnB) * iIB + dot(dj, dj) * (imA + imB);
                     p.dinv[j] = safe_inv(den);
                     V3 wA = A == 0 ? cw1[0] : cw1[1], vA = A == 0 ? cv1[0] : cv1[1];
                     V3 wB = A == 0 ? cw1[1] : cw1[0], vB = A == 0 ? cv1[1] : cv1[0];
-                    float rel = dot(p.rnA[j], wA) + dot(dj, vA) - dot(p.rnB[j], wB) - dot(dj, vB);
+                    float rel = dot(rnA, wA) + dot(dj, vA) - dot(rnB, wB) - dot(dj, vB);
                     p.lam[j] = 0.0f;
                     p.rhs[j] = j == 0 ? normal_rhs(cd.dist, rel, p.dinv[0]) : -rel * p.dinv[j];
                 }
@@ -1243,9 +1246,10 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 wc.store(PS_F_WPPT + 3 * c + 2, lp.z);
             } else {
                 p.a0 = true;
+                p.rA = p.rB = mk(0, 0, 0);
 #pragma unroll
                 for (int j = 0; j < 3; j++) {
-                    p.dir[j] = p.rnA[j] = p.rnB[j] = mk(0, 0, 0);
+                    p.dir[j] = mk(0, 0, 0);
                     p.rhs[j] = p.lam[j] = p.dinv[j] = 0.0f;
                 }
             }
@@ -1253,13 +1257,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
 #pragma unroll
             for (int j = 0; j < 3; j++) {
                 lds.pair(c, 3 * j + 0) = p.dir[j].x; lds.pair(c, 3 * j + 1) = p.dir[j].y; lds.pair(c, 3 * j + 2) = p.dir[j].z;
-                lds.pair(c, 9 + 3 * j + 0) = p.rnA[j].x; lds.pair(c, 9 + 3 * j + 1) = p.rnA[j].y;
-                lds.pair(c, 9 + 3 * j + 2) = p.rnA[j].z;
-                lds.pair(c, 18 + 3 * j + 0) = p.rnB[j].x; lds.pair(c, 18 + 3 * j + 1) = p.rnB[j].y;
-                lds.pair(c, 18 + 3 * j + 2) = p.rnB[j].z;
-                lds.pair(c, 27 + j) = p.rhs[j];
-                lds.pair(c, 30 + j) = p.dinv[j];
+                lds.pair(c, 15 + j) = p.rhs[j];
+                lds.pair(c, 18 + j) = p.dinv[j];
             }
+            lds.pair(c, 9) = p.rA.x; lds.pair(c, 10) = p.rA.y; lds.pair(c, 11) = p.rA.z;
+            lds.pair(c, 12) = p.rB.x; lds.pair(c, 13) = p.rB.y; lds.pair(c, 14) = p.rB.z;
         }
         wc.store(PS_F_WPN, (float)np);
     }
@@ -1352,7 +1354,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         float s = 0.0f;
 #pragma unroll
                         for (int b = 0; b < 9; b++) s += Mi[sidx(a, b)] * c.J[j][b];
-                        lds.at(sl, j, a) = s;
+                        if constexpr (NOBJ != 2) lds.at(sl, j, a) = s;  // Stack rebuilds it in the loop
                         den += c.J[j][a] * s;
                     }
                     float rel = jrow_dot(c.J[j], v1);
@@ -1381,7 +1383,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
 #pragma unroll
                     for (int a = 0; a < 9; a++) {
                         c.J[j][a] = 0.0f;
-                        lds.at(sl, j, a) = 0.0f;
+                        if constexpr (NOBJ != 2) lds.at(sl, j, a) = 0.0f;
                     }
                     c.dir[j] = c.rn[j] = mk(0, 0, 0);
                     c.rhs[j] = c.lam[j] = c.dinv[j] = 0.0f;
@@ -1504,6 +1506,16 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     auto obj_dw = [&](bool o1) { return NOBJ == 2 && o1 ? dw[NB - 1] : dw[0]; };
     auto obj_dv = [&](bool o1) { return NOBJ == 2 && o1 ? dvl[NB - 1] : dvl[0]; };
 
+    // Stack: M^-1 J^T entry a of a gripper row, formed from the M^-1 registers
+    // (its LDS holds the object rows instead)
+    auto mj_of = [&](const float J[9], int a) {
+        float s = 0.0f;
+#pragma unroll
+        for (int b = 0; b < 9; b++) s += Mi[sidx(a, b)] * J[b];
+        return s;
+    };
+    (void)mj_of;
+
     // ---- warm start: the normals that matched a cached contact start from
     // 0.85 x its impulse, applied to the velocity change before the first
     // iteration (btMultiBodyConstraintSolver::setupMultiBodyContactConstraint);
@@ -1533,8 +1545,9 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     bool A1 = !pc[c].a0;
                     float iIA = A1 ? od[NB - 1].iI : od[0].iI, iIB = A1 ? od[0].iI : od[NB - 1].iI;
                     float imA = A1 ? od[NB - 1].inv_m : od[0].inv_m, imB = A1 ? od[0].inv_m : od[NB - 1].inv_m;
-                    obj_add(A1, pv(9) * (l0 * iIA), pv(0) * (l0 * imA));
-                    obj_add(!A1, pv(18) * (-l0 * iIB), pv(0) * (-l0 * imB));
+                    const V3 d0 = pv(0);
+                    obj_add(A1, cross(pv(9), d0) * (l0 * iIA), d0 * (l0 * imA));
+                    obj_add(!A1, cross(pv(12), d0) * (-l0 * iIB), d0 * (-l0 * imB));
                 }
         }
 #pragma unroll
@@ -1543,7 +1556,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 const RobotContact &r = rc[c];
                 const float l0 = r.lam[0];
 #pragma unroll
-                for (int a = 0; a < 9; a++) dv[a] = fmaf(W.at(c, 0, a), l0, dv[a]);
+                for (int a = 0; a < 9; a++) dv[a] = fmaf(NOBJ == 2 ? mj_of(r.J[0], a) : (float)W.at(c, 0, a), l0, dv[a]);
                 if constexpr (NOBJ > 0) {
                     float im = NOBJ == 2 && r.o1 ? od[NB - 1].inv_m : od[0].inv_m;
                     V3 ddw = ANISO ? od[0].inv_inertia(r.rn[0] * -l0)
@@ -1596,16 +1609,17 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     auto pv = [&](int k) { return mk(L.pair(c, k), L.pair(c, k + 1), L.pair(c, k + 2)); };
                     bool A1 = !p.a0;
                     V3 wA = obj_dw(A1), vA = obj_dv(A1), wB = obj_dw(!A1), vB = obj_dv(!A1);
-                    float jv = dot(pv(9), wA) + dot(pv(0), vA) - dot(pv(18), wB) - dot(pv(0), vB);
-                    float dl = (float)L.pair(c, 27) - (float)L.pair(c, 30) * jv;
+                    const V3 d0 = pv(0), rnA = cross(pv(9), d0), rnB = cross(pv(12), d0);
+                    float jv = dot(rnA, wA) + dot(d0, vA) - dot(rnB, wB) - dot(d0, vB);
+                    float dl = (float)L.pair(c, 15) - (float)L.pair(c, 18) * jv;
                     float nl = fminf(fmaxf(p.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
                     dl = nl - p.lam[0];
                     p.lam[0] = nl;
                     float iIA = A1 ? od[NB - 1].iI : od[0].iI, iIB = A1 ? od[0].iI : od[NB - 1].iI;
                     float imA = A1 ? od[NB - 1].inv_m : od[0].inv_m, imB = A1 ? od[0].inv_m : od[NB - 1].inv_m;
-                    obj_add(A1, pv(9) * (dl * iIA), pv(0) * (dl * imA));
-                    obj_add(!A1, pv(18) * (-dl * iIB), pv(0) * (-dl * imB));
-                    res = fmaxf(res, fabsf(dl * res_scale((float)L.pair(c, 30))));
+                    obj_add(A1, rnA * (dl * iIA), d0 * (dl * imA));
+                    obj_add(!A1, rnB * (-dl * iIB), d0 * (-dl * imB));
+                    res = fmaxf(res, fabsf(dl * res_scale((float)L.pair(c, 18))));
                 }
         }
 #pragma unroll
@@ -1615,7 +1629,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 // M^-1 J^T column first: its LDS latency hides under the dot
                 float mj[9];
 #pragma unroll
-                for (int a = 0; a < 9; a++) mj[a] = L.at(c, 0, a);
+                for (int a = 0; a < 9; a++) mj[a] = NOBJ == 2 ? mj_of(r.J[0], a) : (float)L.at(c, 0, a);
                 __builtin_amdgcn_sched_barrier(0);
                 float jv = jrow_dot(r.J[0], dv);
                 if (NOBJ > 0) jv -= dot(r.rn[0], obj_dw(r.o1)) + dot(r.dir[0], obj_dv(r.o1));
@@ -1693,9 +1707,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     auto pv = [&](int k) { return mk(L.pair(c, k), L.pair(c, k + 1), L.pair(c, k + 2)); };
                     bool A1 = !p.a0;
                     V3 wA = obj_dw(A1), vA = obj_dv(A1), wB = obj_dw(!A1), vB = obj_dv(!A1);
-                    float ja = dot(pv(12), wA) + dot(pv(3), vA) - dot(pv(21), wB) - dot(pv(3), vB);
-                    float jb = dot(pv(15), wA) + dot(pv(6), vA) - dot(pv(24), wB) - dot(pv(6), vB);
-                    float dla = (float)L.pair(c, 28) - (float)L.pair(c, 31) * ja, dlb = (float)L.pair(c, 29) - (float)L.pair(c, 32) * jb;
+                    const V3 d1 = pv(3), d2 = pv(6), rA = pv(9), rB = pv(12);
+                    const V3 rnA1 = cross(rA, d1), rnA2 = cross(rA, d2), rnB1 = cross(rB, d1), rnB2 = cross(rB, d2);
+                    float ja = dot(rnA1, wA) + dot(d1, vA) - dot(rnB1, wB) - dot(d1, vB);
+                    float jb = dot(rnA2, wA) + dot(d2, vA) - dot(rnB2, wB) - dot(d2, vB);
+                    float dla = (float)L.pair(c, 16) - (float)L.pair(c, 19) * ja, dlb = (float)L.pair(c, 17) - (float)L.pair(c, 20) * jb;
                     float sa = p.lam[1] + dla, sb = p.lam[2] + dlb;
                     float lim = pmu * fmaxf(p.lam[0], 0.0f);
                     float m2 = sa * sa + sb * sb;
@@ -1708,9 +1724,9 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     p.lam[2] = sb;
                     float iIA = A1 ? od[NB - 1].iI : od[0].iI, iIB = A1 ? od[0].iI : od[NB - 1].iI;
                     float imA = A1 ? od[NB - 1].inv_m : od[0].inv_m, imB = A1 ? od[0].inv_m : od[NB - 1].inv_m;
-                    obj_add(A1, (pv(12) * dla + pv(15) * dlb) * iIA, (pv(3) * dla + pv(6) * dlb) * imA);
-                    obj_add(!A1, (pv(21) * dla + pv(24) * dlb) * -iIB, (pv(3) * dla + pv(6) * dlb) * -imB);
-                    res = fmaxf(res, fmaxf(fabsf(dla * res_scale((float)L.pair(c, 31))), fabsf(dlb * res_scale((float)L.pair(c, 32)))));
+                    obj_add(A1, (rnA1 * dla + rnA2 * dlb) * iIA, (d1 * dla + d2 * dlb) * imA);
+                    obj_add(!A1, (rnB1 * dla + rnB2 * dlb) * -iIB, (d1 * dla + d2 * dlb) * -imB);
+                    res = fmaxf(res, fmaxf(fabsf(dla * res_scale((float)L.pair(c, 19))), fabsf(dlb * res_scale((float)L.pair(c, 20)))));
                 }
         }
 #pragma unroll
@@ -1720,8 +1736,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 float mj1[9], mj2[9];
 #pragma unroll
                 for (int a = 0; a < 9; a++) {
-                    mj1[a] = L.at(c, 1, a);
-                    mj2[a] = L.at(c, 2, a);
+                    mj1[a] = NOBJ == 2 ? mj_of(r.J[1], a) : (float)L.at(c, 1, a);
+                    mj2[a] = NOBJ == 2 ? mj_of(r.J[2], a) : (float)L.at(c, 2, a);
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 float ja = jrow_dot(r.J[1], dv), jb = jrow_dot(r.J[2], dv);
