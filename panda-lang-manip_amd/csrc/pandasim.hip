@@ -21,7 +21,7 @@ struct ps_ctx {
     int device;
     char err[256];
     float *render_prims;  // [B][RENDER_PRIM_FLOATS] scratch of ps_render, allocated on first use
-    float *gstash;        // Stack: [LDS_STASH_FLOATS][stride] substep stash, allocated on first step
+    float *gstash;        // Stack: [GSTASH_FLOATS][stride] substep stash, allocated on first step
     uint8_t *nonfinite;   // ps_set_nonfinite_guard: per-env flag output of ps_step (caller-owned), or NULL
     int reset_nonfinite;  // ... and reset such envs in-kernel
     int lanes_per_env;    // ps_set_lanes_per_env: 0 auto, 1 or 16
@@ -92,7 +92,7 @@ struct KParams {
     int reward_type, block_gripper, obs_dim, action_dim, autoreset;
     uint8_t *nonfinite;  // NaN/Inf guard output (ps_set_nonfinite_guard), NULL = off
     int reset_nonfinite;
-    float *gstash;  // Stack: [LDS_STASH_FLOATS][stride] per-substep stash (ctx scratch)
+    float *gstash;  // Stack: [GSTASH_FLOATS][stride] per-substep stash (ctx scratch)
 };
 
 Scene scene_of(const ps_config &c) {
@@ -1147,7 +1147,7 @@ KParams params_of(ps_ctx *c, void *state) {
 // allocation on the first step of a two-object context, never per step
 int ensure_stash(ps_ctx *c) {
     if (c->cfg.n_objects != 2 || c->gstash) return PS_OK;
-    if (hipMalloc((void **)&c->gstash, sizeof(float) * LDS_STASH_FLOATS * c->lay.stride) != hipSuccess) {
+    if (hipMalloc((void **)&c->gstash, sizeof(float) * GSTASH_FLOATS * c->lay.stride) != hipSuccess) {
         c->gstash = nullptr;
         return PS_ERR_HIP;
     }

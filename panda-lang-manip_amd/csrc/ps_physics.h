@@ -553,21 +553,23 @@ constexpr int LDS_FLOATS = LDS_MI_OFFSET + 45;
 #else
 constexpr int LDS_FLOATS = LDS_MI_OFFSET;
 #endif
-// Stack (two cubes) keeps the read-only data of both cubes' ground rows (r,
-// rhs, dinv: 9 per contact) and of the box-box pair rows (dir[3], rA, rB, rhs,
-// dinv: 21 per contact; the pair rows' r x dir are rebuilt in the loop) in LDS
-// instead of registers, where they spilled ~1.8 KB per lane to scratch beyond
-// L2.  Its gripper rows' M^-1 J^T are not stored: the loop forms them from
-// M^-1 (registers) and J, and its 40-float stash moves to a global per-env
-// buffer (written once and read once per substep, L2-resident).  That is 156
-// floats per lane = 39 KB per 64-lane workgroup: four workgroups per CU, one
-// wave per SIMD, as the one-object scenes.
-constexpr int LDS_GND_OFFSET = 0;
-constexpr int LDS_GND_FLOATS = 9;
-constexpr int LDS_PAIR_OFFSET = LDS_GND_OFFSET + 2 * NG * LDS_GND_FLOATS;
-constexpr int LDS_PAIR_FLOATS = 21;
-constexpr int LDS_FLOATS_STACK = LDS_PAIR_OFFSET + NP * LDS_PAIR_FLOATS;
+// Stack (two cubes) keeps in LDS the gripper rows' J (the slots the other
+// scenes use for M^-1 J^T; the loop forms M^-1 J^T from the M^-1 registers)
+// and both cubes' ground rows (r, rhs: 6 per contact; 1/den is rebuilt from r,
+// cube_ground_dinv) instead of registers, where they spilled to scratch.  Its
+// 40-float stash, object 1's pre-solve state and the box-box pair rows
+// (dir[3], rA, rB, rhs, dinv: 21 per contact, read only while some lane of
+// the wave has a pair contact; r x dir is rebuilt in the loop) sit in a global
+// per-env buffer (GSTASH_FLOATS).  That is 156 LDS floats per lane = 39 KB per
+// 64-lane workgroup: four workgroups per CU, one wave per SIMD, as the
+// one-object scenes.
+constexpr int LDS_GND_OFFSET = NR * 27;
+constexpr int LDS_GND_FLOATS = 6;
+constexpr int LDS_FLOATS_STACK = LDS_GND_OFFSET + 2 * NG * LDS_GND_FLOATS;
 static_assert(LDS_FLOATS_STACK * 4 * 64 * 4 <= 160 * 1024, "four Stack workgroups per CU");
+constexpr int PAIR_FLOATS = 21;
+constexpr int GSTASH_PAIR_OFFSET = LDS_STASH_FLOATS + 13;
+constexpr int GSTASH_FLOATS = GSTASH_PAIR_OFFSET + NP * PAIR_FLOATS;
 template <int NOBJ>
 constexpr int lds_floats() { return NOBJ == 2 ? LDS_FLOATS_STACK : LDS_FLOATS; }
 
@@ -604,14 +606,14 @@ struct MJStore {
     PS_D lds_float &at(int slot, int row, int k) const { return base[((slot * 3 + row) * 9 + k) * stride]; }
     PS_D lds_float &mi(int k) const { return base[(LDS_MI_OFFSET + k) * stride]; }
     PS_D lds_float &stash(int k) const { return base[(LDS_STASH_OFFSET + k) * stride]; }
-    // Stack: the stash in global memory ([LDS_STASH_FLOATS][stride] floats, this env's column)
+    // Stack: the stash in global memory ([GSTASH_FLOATS][stride] floats, this env's column)
     float *gst = nullptr;
     int64_t gst_stride = 0;
     PS_D float &gstash(int k) const { return gst[k * gst_stride]; }
-    // Stack only: ground row c of cube c / NG, field k (r.xyz, rhs[3], dinv[3])
+    // Stack only: ground row c of cube c / NG, field k (r.xyz, rhs[3])
     PS_D lds_float &gnd(int c, int k) const { return base[(LDS_GND_OFFSET + c * LDS_GND_FLOATS + k) * stride]; }
-    // Stack only: pair row c, field k (dir[3].xyz, rA.xyz, rB.xyz, rhs[3], dinv[3])
-    PS_D lds_float &pair(int c, int k) const { return base[(LDS_PAIR_OFFSET + c * LDS_PAIR_FLOATS + k) * stride]; }
+    // Stack only (global stash): pair row c, field k (dir[3].xyz, rA.xyz, rB.xyz, rhs[3], dinv[3])
+    PS_D float &pair(int c, int k) const { return gst[(GSTASH_PAIR_OFFSET + c * PAIR_FLOATS + k) * gst_stride]; }
     // a copy whose address the compiler cannot see through: loads from it are
     // not loop-invariant, so they stay in the PGS loop as ds_reads instead of
     // being hoisted into (spilled) registers
@@ -649,6 +651,14 @@ PS_D float normal_rhs(float dist, float rel, float dinv) {
 }
 
 PS_D float safe_inv(float den) { return den > 2.2204460492503131e-16f ? 1.0f / den : 0.0f; }
+
+// Stack: 1/den of a cube's ground row j (normal +z, then (0,-1,0), (1,0,0))
+// from its contact offset r: den = |r x dir|^2 iI + 1/m (isotropic inertia);
+// the row setup and the solver both use this, so LDS holds r and rhs only
+PS_D float cube_ground_dinv(V3 r, int j, float iI, float inv_m) {
+    V3 rn = j == 0 ? mk(r.y, -r.x, 0.0f) : j == 1 ? mk(r.z, 0.0f, -r.x) : mk(0.0f, r.z, -r.y);
+    return safe_inv(dot(rn, rn * iI) + inv_m);
+}
 
 // Box-box contacts of the two cubes (Stack): the oracle's box_box_contacts
 // (face-axis SAT, incident face clipped against the reference face) in fp32.
@@ -1146,7 +1156,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         V3 rn = cross(r, dirs[j]);
                         V3 w = od[b].inv_inertia(rn);
                         float den = dot(rn, w) + dot(dirs[j], dirs[j]) * od[b].inv_m;
-                        g.dinv[j] = safe_inv(den);
+                        g.dinv[j] = NOBJ == 2 ? cube_ground_dinv(r, j, od[b].iI, od[b].inv_m) : safe_inv(den);
                         float rel = dot(rn, cw1[b]) + dot(dirs[j], cv1[b]);
                         g.lam[j] = 0.0f;
                         g.rhs[j] = j == 0 ? normal_rhs(dist, rel, g.dinv[0]) : -rel * g.dinv[j];
@@ -1158,10 +1168,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         const int at = b * NG + ng[b];
                         lds.gnd(at, 0) = g.r.x; lds.gnd(at, 1) = g.r.y; lds.gnd(at, 2) = g.r.z;
 #pragma unroll
-                        for (int j = 0; j < 3; j++) {
-                            lds.gnd(at, 3 + j) = g.rhs[j];
-                            lds.gnd(at, 6 + j) = g.dinv[j];
-                        }
+                        for (int j = 0; j < 3; j++) lds.gnd(at, 3 + j) = g.rhs[j];
 #pragma unroll
                         for (int s = 0; s < NG; s++)
                             if (s == ng[b]) {
@@ -1253,7 +1260,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     p.rhs[j] = p.lam[j] = p.dinv[j] = 0.0f;
                 }
             }
-            // the read-only part of the row goes to LDS (LDS_PAIR_FLOATS)
+            // the read-only part of the row goes to the global stash (PAIR_FLOATS)
 #pragma unroll
             for (int j = 0; j < 3; j++) {
                 lds.pair(c, 3 * j + 0) = p.dir[j].x; lds.pair(c, 3 * j + 1) = p.dir[j].y; lds.pair(c, 3 * j + 2) = p.dir[j].z;
@@ -1354,7 +1361,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         float s = 0.0f;
 #pragma unroll
                         for (int b = 0; b < 9; b++) s += Mi[sidx(a, b)] * c.J[j][b];
-                        if constexpr (NOBJ != 2) lds.at(sl, j, a) = s;  // Stack rebuilds it in the loop
+                        lds.at(sl, j, a) = NOBJ == 2 ? c.J[j][a] : s;  // Stack: J (M^-1 J^T rebuilt in the loop)
                         den += c.J[j][a] * s;
                     }
                     float rel = jrow_dot(c.J[j], v1);
@@ -1383,7 +1390,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
 #pragma unroll
                     for (int a = 0; a < 9; a++) {
                         c.J[j][a] = 0.0f;
-                        if constexpr (NOBJ != 2) lds.at(sl, j, a) = 0.0f;
+                        lds.at(sl, j, a) = 0.0f;
                     }
                     c.dir[j] = c.rn[j] = mk(0, 0, 0);
                     c.rhs[j] = c.lam[j] = c.dinv[j] = 0.0f;
@@ -1415,6 +1422,12 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         put(30, cv1[0].x); put(31, cv1[0].y); put(32, cv1[0].z);
         put(33, bd[0].pos.x); put(34, bd[0].pos.y); put(35, bd[0].pos.z);
         put(36, bd[0].quat.x); put(37, bd[0].quat.y); put(38, bd[0].quat.z); put(39, bd[0].quat.w);
+    }
+    if constexpr (NOBJ == 2) {
+        put(40, cw1[1].x); put(41, cw1[1].y); put(42, cw1[1].z);
+        put(43, cv1[1].x); put(44, cv1[1].y); put(45, cv1[1].z);
+        put(46, bd[1].pos.x); put(47, bd[1].pos.y); put(48, bd[1].pos.z);
+        put(49, bd[1].quat.x); put(50, bd[1].quat.y); put(51, bd[1].quat.z); put(52, bd[1].quat.w);
     }
 
     // ---- projected Gauss-Seidel
@@ -1555,8 +1568,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             if (gate_robot & (1u << c)) {
                 const RobotContact &r = rc[c];
                 const float l0 = r.lam[0];
+                float Jl[9];
 #pragma unroll
-                for (int a = 0; a < 9; a++) dv[a] = fmaf(NOBJ == 2 ? mj_of(r.J[0], a) : (float)W.at(c, 0, a), l0, dv[a]);
+                for (int a = 0; a < 9; a++) Jl[a] = NOBJ == 2 ? (float)W.at(c, 0, a) : r.J[0][a];
+#pragma unroll
+                for (int a = 0; a < 9; a++) dv[a] = fmaf(NOBJ == 2 ? mj_of(Jl, a) : (float)W.at(c, 0, a), l0, dv[a]);
                 if constexpr (NOBJ > 0) {
                     float im = NOBJ == 2 && r.o1 ? od[NB - 1].inv_m : od[0].inv_m;
                     V3 ddw = ANISO ? od[0].inv_inertia(r.rn[0] * -l0)
@@ -1581,7 +1597,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         const int at = b * NG + c;
                         gr = mk(L.gnd(at, 0), L.gnd(at, 1), L.gnd(at, 2));
                         grhs = L.gnd(at, 3);
-                        gdinv = L.gnd(at, 6);
+                        gdinv = cube_ground_dinv(gr, 0, od[b].iI, inv_m);
                     }
                     V3 rn = mk(gr.y, -gr.x, 0.0f);  // r x (0,0,1); zero terms dropped below
                     float dl = grhs - gdinv * (rn.x * dw[b].x + rn.y * dw[b].y + dvl[b].z);
@@ -1605,7 +1621,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             for (int c = 0; c < NP; c++)
                 if (gate_pair & (1u << c)) {
                     PairContact &p = pc[c];
-                    // Stack: the row's read-only data come from LDS (LDS_PAIR_FLOATS)
+                    // Stack: the row's read-only data come from the global stash (PAIR_FLOATS)
                     auto pv = [&](int k) { return mk(L.pair(c, k), L.pair(c, k + 1), L.pair(c, k + 2)); };
                     bool A1 = !p.a0;
                     V3 wA = obj_dw(A1), vA = obj_dv(A1), wB = obj_dw(!A1), vB = obj_dv(!A1);
@@ -1627,11 +1643,13 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             if (gate_robot & (1u << c)) {
                 RobotContact &r = rc[c];
                 // M^-1 J^T column first: its LDS latency hides under the dot
-                float mj[9];
+                float mj[9], Jl[9];
 #pragma unroll
-                for (int a = 0; a < 9; a++) mj[a] = NOBJ == 2 ? mj_of(r.J[0], a) : (float)L.at(c, 0, a);
+                for (int a = 0; a < 9; a++) Jl[a] = NOBJ == 2 ? (float)L.at(c, 0, a) : r.J[0][a];
+#pragma unroll
+                for (int a = 0; a < 9; a++) mj[a] = NOBJ == 2 ? mj_of(Jl, a) : (float)L.at(c, 0, a);
                 __builtin_amdgcn_sched_barrier(0);
-                float jv = jrow_dot(r.J[0], dv);
+                float jv = jrow_dot(Jl, dv);
                 if (NOBJ > 0) jv -= dot(r.rn[0], obj_dw(r.o1)) + dot(r.dir[0], obj_dv(r.o1));
                 float dl = r.rhs[0] - r.dinv[0] * jv;
                 float nl = fminf(fmaxf(r.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
@@ -1665,8 +1683,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         gr = mk(L.gnd(at, 0), L.gnd(at, 1), L.gnd(at, 2));
                         grhs1 = L.gnd(at, 4);
                         grhs2 = L.gnd(at, 5);
-                        gdinv1 = L.gnd(at, 7);
-                        gdinv2 = L.gnd(at, 8);
+                        gdinv1 = cube_ground_dinv(gr, 1, od[b].iI, inv_m);
+                        gdinv2 = cube_ground_dinv(gr, 2, od[b].iI, inv_m);
                     }
                     V3 r1 = mk(gr.z, 0.0f, -gr.x);  // r x (0,-1,0)
                     V3 r2 = mk(0.0f, gr.z, -gr.y);  // r x (1,0,0)
@@ -1703,7 +1721,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             for (int c = 0; c < NP; c++)
                 if (gate_pair & (1u << c)) {
                     PairContact &p = pc[c];
-                    // Stack: the row's read-only data come from LDS (LDS_PAIR_FLOATS)
+                    // Stack: the row's read-only data come from the global stash (PAIR_FLOATS)
                     auto pv = [&](int k) { return mk(L.pair(c, k), L.pair(c, k + 1), L.pair(c, k + 2)); };
                     bool A1 = !p.a0;
                     V3 wA = obj_dw(A1), vA = obj_dv(A1), wB = obj_dw(!A1), vB = obj_dv(!A1);
@@ -1733,14 +1751,19 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         for (int c = 0; c < NR; c++)
             if (gate_robot & (1u << c)) {
                 RobotContact &r = rc[c];
-                float mj1[9], mj2[9];
+                float mj1[9], mj2[9], J1[9], J2[9];
 #pragma unroll
                 for (int a = 0; a < 9; a++) {
-                    mj1[a] = NOBJ == 2 ? mj_of(r.J[1], a) : (float)L.at(c, 1, a);
-                    mj2[a] = NOBJ == 2 ? mj_of(r.J[2], a) : (float)L.at(c, 2, a);
+                    J1[a] = NOBJ == 2 ? (float)L.at(c, 1, a) : r.J[1][a];
+                    J2[a] = NOBJ == 2 ? (float)L.at(c, 2, a) : r.J[2][a];
+                }
+#pragma unroll
+                for (int a = 0; a < 9; a++) {
+                    mj1[a] = NOBJ == 2 ? mj_of(J1, a) : (float)L.at(c, 1, a);
+                    mj2[a] = NOBJ == 2 ? mj_of(J2, a) : (float)L.at(c, 2, a);
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                float ja = jrow_dot(r.J[1], dv), jb = jrow_dot(r.J[2], dv);
+                float ja = jrow_dot(J1, dv), jb = jrow_dot(J2, dv);
                 if (NOBJ > 0) {
                     V3 ow = obj_dw(r.o1), ov = obj_dv(r.o1);
                     ja -= dot(r.rn[1], ow) + dot(r.dir[1], ov);
@@ -1862,6 +1885,12 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             cv1[0] = mk(get(S, 30), get(S, 31), get(S, 32));
             bd[0].pos = mk(get(S, 33), get(S, 34), get(S, 35));
             bd[0].quat = Q4{get(S, 36), get(S, 37), get(S, 38), get(S, 39)};
+        }
+        if constexpr (NOBJ == 2) {
+            cw1[1] = mk(get(S, 40), get(S, 41), get(S, 42));
+            cv1[1] = mk(get(S, 43), get(S, 44), get(S, 45));
+            bd[1].pos = mk(get(S, 46), get(S, 47), get(S, 48));
+            bd[1].quat = Q4{get(S, 49), get(S, 50), get(S, 51), get(S, 52)};
         }
     }
     // ---- integrate (btMultiBody::stepPositionsMultiDof)
