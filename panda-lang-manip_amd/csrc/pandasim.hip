@@ -21,7 +21,7 @@ struct ps_ctx {
     int device;
     char err[256];
     float *render_prims;  // [B][RENDER_PRIM_FLOATS] scratch of ps_render, allocated on first use
-    float *gstash;        // Stack: [GSTASH_FLOATS][stride] substep stash, allocated on first step
+    float *gstash;        // Stack: GSTASH_FLOATS x stride substep stash and pair rows, allocated on first step
     uint8_t *nonfinite;   // ps_set_nonfinite_guard: per-env flag output of ps_step (caller-owned), or NULL
     int reset_nonfinite;  // ... and reset such envs in-kernel
     int lanes_per_env;    // ps_set_lanes_per_env: 0 auto, 1 or 16
@@ -92,7 +92,7 @@ struct KParams {
     int reward_type, block_gripper, obs_dim, action_dim, autoreset;
     uint8_t *nonfinite;  // NaN/Inf guard output (ps_set_nonfinite_guard), NULL = off
     int reset_nonfinite;
-    float *gstash;  // Stack: [GSTASH_FLOATS][stride] per-substep stash (ctx scratch)
+    float *gstash;  // Stack: GSTASH_FLOATS x stride per-substep stash and pair rows (ctx scratch)
 };
 
 Scene scene_of(const ps_config &c) {
@@ -522,6 +522,8 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
     if constexpr (T::NOBJ == 2) {
         lds.gst = P.gstash + i;
         lds.gst_stride = s.stride;
+        lds.gpair = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_PAIR_OFFSET * s.stride +
+                                                                 i * (NP * PAIR_FLOATS));
     }
     run_substeps<T::NOBJ, T::SHAPE, true, G>(P, i, PM_SUBSTEPS, q, qd, bd, lds, live PS_PROF_ARG);
     double g[6] = {0, 0, 0, 0, 0, 0};
@@ -602,6 +604,8 @@ __global__ __launch_bounds__(kBlock) void k_sim_step(KParams P, int n_substeps) 
     if constexpr (NOBJ == 2) {
         lds.gst = P.gstash + i;
         lds.gst_stride = s.stride;
+        lds.gpair = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_PAIR_OFFSET * s.stride +
+                                                                 i * (NP * PAIR_FLOATS));
     }
 #ifdef PS_PROFILE_PHASES
     PhaseTimer pt;

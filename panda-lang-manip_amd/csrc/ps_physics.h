@@ -560,7 +560,8 @@ constexpr int LDS_FLOATS = LDS_MI_OFFSET;
 // 40-float stash, object 1's pre-solve state and the box-box pair rows
 // (dir[3], rA, rB, rhs, dinv: 21 per contact, read only while some lane of
 // the wave has a pair contact; r x dir is rebuilt in the loop) sit in a global
-// per-env buffer (GSTASH_FLOATS).  That is 156 LDS floats per lane = 39 KB per
+// per-env buffer (GSTASH_FLOATS: the stash rows env-minor, the pair rows
+// env-major so one lane pointer with immediate offsets reads them).  That is 156 LDS floats per lane = 39 KB per
 // 64-lane workgroup: four workgroups per CU, one wave per SIMD, as the
 // one-object scenes.
 constexpr int LDS_GND_OFFSET = NR * 27;
@@ -584,7 +585,7 @@ struct GroundContact {
 
 // object-object contact (Stack): A = incident body (+n), B = reference (-n)
 struct PairContact {
-    V3 dir[3], rA, rB;  // rA, rB: contact point - COM of A, B
+    V3 dir[3], rA, rB;  // contact point - COM of object 0 (rA) and of object 1 (rB)
     float rhs[3], lam[3], dinv[3];
     bool a0;  // body A is object 0
 };
@@ -606,14 +607,18 @@ struct MJStore {
     PS_D lds_float &at(int slot, int row, int k) const { return base[((slot * 3 + row) * 9 + k) * stride]; }
     PS_D lds_float &mi(int k) const { return base[(LDS_MI_OFFSET + k) * stride]; }
     PS_D lds_float &stash(int k) const { return base[(LDS_STASH_OFFSET + k) * stride]; }
-    // Stack: the stash in global memory ([GSTASH_FLOATS][stride] floats, this env's column)
+    // Stack: the stash in global memory ([GSTASH_PAIR_OFFSET][stride] floats, this env's column)
     float *gst = nullptr;
     int64_t gst_stride = 0;
+    // Stack: this env's pair rows, env-major after the stash rows
+    // ([stride][NP * PAIR_FLOATS]): one lane pointer plus immediate offsets
+    __attribute__((address_space(1))) float *gpair = nullptr;
     PS_D float &gstash(int k) const { return gst[k * gst_stride]; }
     // Stack only: ground row c of cube c / NG, field k (r.xyz, rhs[3])
     PS_D lds_float &gnd(int c, int k) const { return base[(LDS_GND_OFFSET + c * LDS_GND_FLOATS + k) * stride]; }
-    // Stack only (global stash): pair row c, field k (dir[3].xyz, rA.xyz, rB.xyz, rhs[3], dinv[3])
-    PS_D float &pair(int c, int k) const { return gst[(GSTASH_PAIR_OFFSET + c * PAIR_FLOATS + k) * gst_stride]; }
+    // Stack only (global stash): pair row c, field k (dir[3].xyz, r0.xyz, r1.xyz, rhs[3], dinv[3]);
+    // dir is body A's (+n), r0 / r1 are the offsets from object 0 / 1
+    PS_D float &pair(int c, int k) const { return *(float *)&gpair[c * PAIR_FLOATS + k]; }
     // a copy whose address the compiler cannot see through: loads from it are
     // not loop-invariant, so they stay in the PGS loop as ds_reads instead of
     // being hoisted into (spilled) registers
@@ -621,6 +626,7 @@ struct MJStore {
         MJStore r = *this;
         asm volatile("" : "+v"(r.base));
         asm volatile("" : "+v"(r.gst));
+        asm volatile("" : "+v"(r.gpair));
         return r;
     }
 };
@@ -657,7 +663,7 @@ PS_D float safe_inv(float den) { return den > 2.2204460492503131e-16f ? 1.0f / d
 // the row setup and the solver both use this, so LDS holds r and rhs only
 PS_D float cube_ground_dinv(V3 r, int j, float iI, float inv_m) {
     V3 rn = j == 0 ? mk(r.y, -r.x, 0.0f) : j == 1 ? mk(r.z, 0.0f, -r.x) : mk(0.0f, r.z, -r.y);
-    return safe_inv(dot(rn, rn * iI) + inv_m);
+    return __builtin_amdgcn_rcpf(dot(rn, rn * iI) + inv_m);  // den >= 1/m > 0
 }
 
 // Box-box contacts of the two cubes (Stack): the oracle's box_box_contacts
@@ -769,7 +775,15 @@ PS_D int box_box(const Scene &sc, const Body &b0, const Body &b1, const M3 &R0, 
 // there (the reference skips such rows), never 0 * inf = NaN -- a NaN in the
 // residual max would depend on fmaxf's NaN rule, which a build that assumes
 // no NaNs is free to change.
-PS_D float res_scale(float dinv) { return __builtin_amdgcn_rcpf(fmaxf(dinv, 1.17549435e-38f)); }
+// PGS stopping rule: Bullet stops once max over rows of (dl / dinv)^2 <= 1e-7
+// (the residual is the impulse change times the row's effective mass).  The
+// loop tracks it as a violation that is <= 0 once every row has
+// |dl| / dinv <= sqrt(1e-7), so no row takes a reciprocal:
+//   contact rows  |dl| - sqrt(1e-7) dinv
+//   joint rows    |dl| den - sqrt(1e-7)      (den = M^-1_dd, in registers)
+constexpr float kResidualAbs = 3.16227766e-4f;
+PS_D float row_viol(float dl, float dinv) { return fmaf(-kResidualAbs, dinv, fabsf(dl)); }
+PS_D float joint_viol(float dl, float den) { return fmaf(fabsf(dl), den, -kResidualAbs); }
 
 // The warm start's contact cache (state rows PS_F_WG0.. of this env, see
 // include/pandasim.h): read at contact generation, written after the solve.
@@ -905,7 +919,7 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         dl = nl - lam;
         lam = nl;
         dvm = fmaf(mrow[d], sgn * dl, dvm);
-        res = fmaxf(res, fabsf(dl * midg[d]));
+        res = fmaxf(res, joint_viol(dl, midg[d]));
     };
     auto limit_row = [&](auto DD) {
         constexpr int d = decltype(DD)::value;
@@ -930,7 +944,7 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         dl = nl - lam;
         lam = nl;
         dvm = fmaf(Mm, dl, dvm);
-        res = fmaxf(res, fabsf(dl * res_scale(dinv)));
+        res = fmaxf(res, row_viol(dl, dinv));
     };
     auto cone = [&](const float J[3], const float M[3], const float rhs[3], const float dinv[3], float lam[3],
                     float mu) {
@@ -946,7 +960,7 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         lam[1] = a;
         lam[2] = b;
         dvm = fmaf(M[2], dlb, fmaf(M[1], dla, dvm));
-        res = fmaxf(res, fmaxf(fabsf(dla * res_scale(dinv[1])), fabsf(dlb * res_scale(dinv[2]))));
+        res = fmaxf(res, fmaxf(row_viol(dla, dinv[1]), row_viol(dlb, dinv[2])));
     };
     auto contacts = [&]() {
 #pragma unroll
@@ -962,7 +976,6 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         for (int c = 0; c < NR; c++)
             if (gate_robot & (1u << c)) cone(rJ[c], rM[c], rc[c].rhs, rc[c].dinv, rc[c].lam, rc[c].mu);
     };
-    constexpr float kResidualAbs = 3.16227766e-4f;
     for (int it = 0; it < PM_SOLVER_ITERATIONS; it += 2) {
 #ifdef PS_PROFILE_PHASES
         prof_it++;
@@ -971,7 +984,7 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         down(motor_row);
         if (gate_lim != 0u) down(limit_row);
         contacts();
-        if (res <= kResidualAbs) break;
+        if (res <= 0.0f) break;
 #ifdef PS_PROFILE_PHASES
         prof_it++;
 #endif
@@ -979,7 +992,7 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         if (gate_lim != 0u) up(limit_row);
         up(motor_row);
         contacts();
-        if (res <= kResidualAbs) break;
+        if (res <= 0.0f) break;
     }
     // every lane of the group gets the whole velocity change
 #pragma unroll
@@ -1220,8 +1233,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 plane_space(cd.n, dirs[1], dirs[2]);
                 V3 rA = cd.pA - (A == 0 ? bd[0].pos : bd[1].pos), rB = cd.pB - (A == 0 ? bd[1].pos : bd[0].pos);
                 p.a0 = cd.a0;
-                p.rA = rA;
-                p.rB = rB;
+                p.rA = A == 0 ? rA : rB;  // stored by object index: offset from object 0's COM
+                p.rB = A == 0 ? rB : rA;  // and from object 1's
 #pragma unroll
                 for (int j = 0; j < 3; j++) {
                     V3 dj = dirs[j];
@@ -1471,9 +1484,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
 #else
 #define PS_COUNT_IT() do {} while (0)
 #endif
-    // the solver stops when max(residual^2) <= 1e-7; tracked as max |residual|
-    // (one v_max with an abs modifier per row) against sqrt(1e-7)
-    constexpr float kResidualAbs = 3.16227766e-4f;
+    // the solver stops when every row's violation (row_viol, joint_viol) is <= 0
     static_assert(PM_SOLVER_ITERATIONS % 2 == 0, "iteration pairs");
     if constexpr (G == 1) {
     auto joint_row = [&](int d, float sgn, float rhs, float &lam, float lo, float hi) {
@@ -1489,8 +1500,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
 #pragma unroll
             for (int a = 0; a < 9; a++) dv[a] += L.mi(sidx(a, d)) * f;
         }
-        float x = dl * (MI_REGS ? Mi[sidx(d, d)] : (float)L.mi(sidx(d, d)));  // residual dl / dinv
-        res = fmaxf(res, fabsf(x));
+        res = fmaxf(res, joint_viol(dl, MI_REGS ? Mi[sidx(d, d)] : (float)L.mi(sidx(d, d))));
     };
     auto limit_row = [&](int d) {
         if (gate_lim & (1u << d)) {
@@ -1507,10 +1517,13 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     // other scenes have one object and the select folds away)
     auto obj_add = [&](bool o1, V3 ddw, V3 ddv) {
         if constexpr (NOBJ == 2) {
-            dw[0] = dw[0] + (o1 ? mk(0, 0, 0) : ddw);
-            dvl[0] = dvl[0] + (o1 ? mk(0, 0, 0) : ddv);
-            dw[NB - 1] = dw[NB - 1] + (o1 ? ddw : mk(0, 0, 0));
-            dvl[NB - 1] = dvl[NB - 1] + (o1 ? ddv : mk(0, 0, 0));
+            // a 0/1 weight per object: one FMA per component instead of a
+            // select and an add
+            const float s1 = o1 ? 1.0f : 0.0f, s0 = o1 ? 0.0f : 1.0f;
+            dw[0] = fma3(ddw, s0, dw[0]);
+            dvl[0] = fma3(ddv, s0, dvl[0]);
+            dw[NB - 1] = fma3(ddw, s1, dw[NB - 1]);
+            dvl[NB - 1] = fma3(ddv, s1, dvl[NB - 1]);
         } else {
             dw[0] = dw[0] + ddw;
             dvl[0] = dvl[0] + ddv;
@@ -1518,16 +1531,34 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     };
     auto obj_dw = [&](bool o1) { return NOBJ == 2 && o1 ? dw[NB - 1] : dw[0]; };
     auto obj_dv = [&](bool o1) { return NOBJ == 2 && o1 ? dvl[NB - 1] : dvl[0]; };
-
-    // Stack: M^-1 J^T entry a of a gripper row, formed from the M^-1 registers
-    // (its LDS holds the object rows instead)
-    auto mj_of = [&](const float J[9], int a) {
-        float s = 0.0f;
-#pragma unroll
-        for (int b = 0; b < 9; b++) s += Mi[sidx(a, b)] * J[b];
-        return s;
+    // Stack pair rows in the objects' own frame: with rn0 = r0 x d, rn1 = r1 x d
+    // the row velocity is sg * pair_rel (sg = +1 when body A is object 0), and
+    // an impulse dl on A moves object 0 by +sg dl and object 1 by -sg dl
+    auto pair_rel = [&](V3 rn0, V3 rn1, V3 d) {
+        return dot(rn0, dw[0]) + dot(d, dvl[0]) - dot(rn1, dw[NB - 1]) - dot(d, dvl[NB - 1]);
     };
-    (void)mj_of;
+    auto pair_apply = [&](V3 rn0, V3 rn1, V3 d, float sdl) {
+        dw[0] = fma3(rn0, sdl * od[0].iI, dw[0]);
+        dvl[0] = fma3(d, sdl * od[0].inv_m, dvl[0]);
+        dw[NB - 1] = fma3(rn1, -sdl * od[NB - 1].iI, dw[NB - 1]);
+        dvl[NB - 1] = fma3(d, -sdl * od[NB - 1].inv_m, dvl[NB - 1]);
+    };
+    (void)pair_rel;
+    (void)pair_apply;
+
+    // Stack keeps the gripper rows' J, not M^-1 J^T, in LDS: dv += M^-1 g for
+    // the generalized impulse g (J^T dl, or both friction rows' J^T dl summed:
+    // one product with the M^-1 registers per contact and sweep)
+    auto mi_apply = [&](const float g[9]) {
+#pragma unroll
+        for (int a = 0; a < 9; a++) {
+            float s = dv[a];
+#pragma unroll
+            for (int b = 0; b < 9; b++) s = fmaf(Mi[sidx(a, b)], g[b], s);
+            dv[a] = s;
+        }
+    };
+    (void)mi_apply;
 
     // ---- warm start: the normals that matched a cached contact start from
     // 0.85 x its impulse, applied to the velocity change before the first
@@ -1553,14 +1584,10 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
 #pragma unroll
             for (int c = 0; c < NP; c++)
                 if (gate_pair & (1u << c)) {
-                    const float l0 = pc[c].lam[0];
                     auto pv = [&](int k) { return mk(W.pair(c, k), W.pair(c, k + 1), W.pair(c, k + 2)); };
-                    bool A1 = !pc[c].a0;
-                    float iIA = A1 ? od[NB - 1].iI : od[0].iI, iIB = A1 ? od[0].iI : od[NB - 1].iI;
-                    float imA = A1 ? od[NB - 1].inv_m : od[0].inv_m, imB = A1 ? od[0].inv_m : od[NB - 1].inv_m;
+                    const float sl = pc[c].a0 ? pc[c].lam[0] : -pc[c].lam[0];
                     const V3 d0 = pv(0);
-                    obj_add(A1, cross(pv(9), d0) * (l0 * iIA), d0 * (l0 * imA));
-                    obj_add(!A1, cross(pv(12), d0) * (-l0 * iIB), d0 * (-l0 * imB));
+                    pair_apply(cross(pv(9), d0), cross(pv(12), d0), d0, sl);
                 }
         }
 #pragma unroll
@@ -1571,8 +1598,15 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 float Jl[9];
 #pragma unroll
                 for (int a = 0; a < 9; a++) Jl[a] = NOBJ == 2 ? (float)W.at(c, 0, a) : r.J[0][a];
+                if constexpr (NOBJ == 2) {
+                    float g[9];
 #pragma unroll
-                for (int a = 0; a < 9; a++) dv[a] = fmaf(NOBJ == 2 ? mj_of(Jl, a) : (float)W.at(c, 0, a), l0, dv[a]);
+                    for (int a = 0; a < 9; a++) g[a] = Jl[a] * l0;
+                    mi_apply(g);
+                } else {
+#pragma unroll
+                    for (int a = 0; a < 9; a++) dv[a] = fmaf(W.at(c, 0, a), l0, dv[a]);
+                }
                 if constexpr (NOBJ > 0) {
                     float im = NOBJ == 2 && r.o1 ? od[NB - 1].inv_m : od[0].inv_m;
                     V3 ddw = ANISO ? od[0].inv_inertia(r.rn[0] * -l0)
@@ -1613,7 +1647,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         dw[b].y = fmaf(rn.y, dI, dw[b].y);
                     }
                     dvl[b].z = fmaf(dl, inv_m, dvl[b].z);
-                    res = fmaxf(res, fabsf(dl * res_scale(gdinv)));
+                    res = fmaxf(res, row_viol(dl, gdinv));
                 }
         }
         if constexpr (NOBJ == 2) {
@@ -1623,19 +1657,15 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     PairContact &p = pc[c];
                     // Stack: the row's read-only data come from the global stash (PAIR_FLOATS)
                     auto pv = [&](int k) { return mk(L.pair(c, k), L.pair(c, k + 1), L.pair(c, k + 2)); };
-                    bool A1 = !p.a0;
-                    V3 wA = obj_dw(A1), vA = obj_dv(A1), wB = obj_dw(!A1), vB = obj_dv(!A1);
-                    const V3 d0 = pv(0), rnA = cross(pv(9), d0), rnB = cross(pv(12), d0);
-                    float jv = dot(rnA, wA) + dot(d0, vA) - dot(rnB, wB) - dot(d0, vB);
+                    const float sg = p.a0 ? 1.0f : -1.0f;  // A = object 0: +1
+                    const V3 d0 = pv(0), rn0 = cross(pv(9), d0), rn1 = cross(pv(12), d0);
+                    float jv = sg * pair_rel(rn0, rn1, d0);
                     float dl = (float)L.pair(c, 15) - (float)L.pair(c, 18) * jv;
                     float nl = fminf(fmaxf(p.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
                     dl = nl - p.lam[0];
                     p.lam[0] = nl;
-                    float iIA = A1 ? od[NB - 1].iI : od[0].iI, iIB = A1 ? od[0].iI : od[NB - 1].iI;
-                    float imA = A1 ? od[NB - 1].inv_m : od[0].inv_m, imB = A1 ? od[0].inv_m : od[NB - 1].inv_m;
-                    obj_add(A1, rnA * (dl * iIA), d0 * (dl * imA));
-                    obj_add(!A1, rnB * (-dl * iIB), d0 * (-dl * imB));
-                    res = fmaxf(res, fabsf(dl * res_scale((float)L.pair(c, 18))));
+                    pair_apply(rn0, rn1, d0, sg * dl);
+                    res = fmaxf(res, row_viol(dl, L.pair(c, 18)));
                 }
         }
 #pragma unroll
@@ -1646,8 +1676,10 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 float mj[9], Jl[9];
 #pragma unroll
                 for (int a = 0; a < 9; a++) Jl[a] = NOBJ == 2 ? (float)L.at(c, 0, a) : r.J[0][a];
+                if constexpr (NOBJ != 2) {
 #pragma unroll
-                for (int a = 0; a < 9; a++) mj[a] = NOBJ == 2 ? mj_of(Jl, a) : (float)L.at(c, 0, a);
+                    for (int a = 0; a < 9; a++) mj[a] = L.at(c, 0, a);
+                }
                 __builtin_amdgcn_sched_barrier(0);
                 float jv = jrow_dot(Jl, dv);
                 if (NOBJ > 0) jv -= dot(r.rn[0], obj_dw(r.o1)) + dot(r.dir[0], obj_dv(r.o1));
@@ -1655,8 +1687,15 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 float nl = fminf(fmaxf(r.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
                 dl = nl - r.lam[0];
                 r.lam[0] = nl;
+                if constexpr (NOBJ == 2) {
+                    float g[9];
 #pragma unroll
-                for (int a = 0; a < 9; a++) dv[a] = fmaf(mj[a], dl, dv[a]);
+                    for (int a = 0; a < 9; a++) g[a] = Jl[a] * dl;
+                    mi_apply(g);
+                } else {
+#pragma unroll
+                    for (int a = 0; a < 9; a++) dv[a] = fmaf(mj[a], dl, dv[a]);
+                }
                 if constexpr (NOBJ == 1) {
                     // one object: fma straight into its velocity change
                     dw[0] = ANISO ? dw[0] + od[0].inv_inertia(r.rn[0] * -dl) : fma3(r.rn[0], -dl * od[0].iI, dw[0]);
@@ -1666,7 +1705,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     float iI = r.o1 ? od[NB - 1].iI : od[0].iI;
                     obj_add(r.o1, r.rn[0] * (-dl * iI), r.dir[0] * (-dl * im));
                 }
-                res = fmaxf(res, fabsf(dl * res_scale(r.dinv[0])));
+                res = fmaxf(res, row_viol(dl, r.dinv[0]));
             }
         // friction cones
 #pragma unroll
@@ -1712,7 +1751,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     }
                     dvl[b].x = fmaf(dlb, inv_m, dvl[b].x);
                     dvl[b].y = fmaf(-dla, inv_m, dvl[b].y);
-                    res = fmaxf(res, fmaxf(fabsf(dla * res_scale(gdinv1)), fabsf(dlb * res_scale(gdinv2))));
+                    res = fmaxf(res, fmaxf(row_viol(dla, gdinv1), row_viol(dlb, gdinv2)));
                 }
         }
         if constexpr (NOBJ == 2) {
@@ -1723,12 +1762,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     PairContact &p = pc[c];
                     // Stack: the row's read-only data come from the global stash (PAIR_FLOATS)
                     auto pv = [&](int k) { return mk(L.pair(c, k), L.pair(c, k + 1), L.pair(c, k + 2)); };
-                    bool A1 = !p.a0;
-                    V3 wA = obj_dw(A1), vA = obj_dv(A1), wB = obj_dw(!A1), vB = obj_dv(!A1);
-                    const V3 d1 = pv(3), d2 = pv(6), rA = pv(9), rB = pv(12);
-                    const V3 rnA1 = cross(rA, d1), rnA2 = cross(rA, d2), rnB1 = cross(rB, d1), rnB2 = cross(rB, d2);
-                    float ja = dot(rnA1, wA) + dot(d1, vA) - dot(rnB1, wB) - dot(d1, vB);
-                    float jb = dot(rnA2, wA) + dot(d2, vA) - dot(rnB2, wB) - dot(d2, vB);
+                    const float sg = p.a0 ? 1.0f : -1.0f;
+                    const V3 d1 = pv(3), d2 = pv(6), r0 = pv(9), r1 = pv(12);
+                    const V3 rn01 = cross(r0, d1), rn02 = cross(r0, d2), rn11 = cross(r1, d1), rn12 = cross(r1, d2);
+                    float ja = sg * pair_rel(rn01, rn11, d1);
+                    float jb = sg * pair_rel(rn02, rn12, d2);
                     float dla = (float)L.pair(c, 16) - (float)L.pair(c, 19) * ja, dlb = (float)L.pair(c, 17) - (float)L.pair(c, 20) * jb;
                     float sa = p.lam[1] + dla, sb = p.lam[2] + dlb;
                     float lim = pmu * fmaxf(p.lam[0], 0.0f);
@@ -1740,11 +1778,9 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     dlb = sb - p.lam[2];
                     p.lam[1] = sa;
                     p.lam[2] = sb;
-                    float iIA = A1 ? od[NB - 1].iI : od[0].iI, iIB = A1 ? od[0].iI : od[NB - 1].iI;
-                    float imA = A1 ? od[NB - 1].inv_m : od[0].inv_m, imB = A1 ? od[0].inv_m : od[NB - 1].inv_m;
-                    obj_add(A1, (rnA1 * dla + rnA2 * dlb) * iIA, (d1 * dla + d2 * dlb) * imA);
-                    obj_add(!A1, (rnB1 * dla + rnB2 * dlb) * -iIB, (d1 * dla + d2 * dlb) * -imB);
-                    res = fmaxf(res, fmaxf(fabsf(dla * res_scale((float)L.pair(c, 19))), fabsf(dlb * res_scale((float)L.pair(c, 20)))));
+                    pair_apply(rn01, rn11, d1, sg * dla);
+                    pair_apply(rn02, rn12, d2, sg * dlb);
+                    res = fmaxf(res, fmaxf(row_viol(dla, L.pair(c, 19)), row_viol(dlb, L.pair(c, 20))));
                 }
         }
 #pragma unroll
@@ -1757,10 +1793,12 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     J1[a] = NOBJ == 2 ? (float)L.at(c, 1, a) : r.J[1][a];
                     J2[a] = NOBJ == 2 ? (float)L.at(c, 2, a) : r.J[2][a];
                 }
+                if constexpr (NOBJ != 2) {
 #pragma unroll
-                for (int a = 0; a < 9; a++) {
-                    mj1[a] = NOBJ == 2 ? mj_of(J1, a) : (float)L.at(c, 1, a);
-                    mj2[a] = NOBJ == 2 ? mj_of(J2, a) : (float)L.at(c, 2, a);
+                    for (int a = 0; a < 9; a++) {
+                        mj1[a] = L.at(c, 1, a);
+                        mj2[a] = L.at(c, 2, a);
+                    }
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 float ja = jrow_dot(J1, dv), jb = jrow_dot(J2, dv);
@@ -1780,8 +1818,15 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 dlb = sb - r.lam[2];
                 r.lam[1] = sa;
                 r.lam[2] = sb;
+                if constexpr (NOBJ == 2) {
+                    float g[9];
 #pragma unroll
-                for (int a = 0; a < 9; a++) dv[a] = fmaf(mj2[a], dlb, fmaf(mj1[a], dla, dv[a]));
+                    for (int a = 0; a < 9; a++) g[a] = fmaf(J2[a], dlb, J1[a] * dla);
+                    mi_apply(g);
+                } else {
+#pragma unroll
+                    for (int a = 0; a < 9; a++) dv[a] = fmaf(mj2[a], dlb, fmaf(mj1[a], dla, dv[a]));
+                }
                 if constexpr (NOBJ == 1) {
                     if constexpr (ANISO) {
                         dw[0] = dw[0] + od[0].inv_inertia(fma3(r.rn[2], -dlb, r.rn[1] * -dla));
@@ -1803,7 +1848,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                                 fmaf(r.dir[2].z, bm, r.dir[1].z * am));
                     obj_add(r.o1, ddw, ddv);
                 }
-                res = fmaxf(res, fmaxf(fabsf(dla * res_scale(r.dinv[1])), fabsf(dlb * res_scale(r.dinv[2]))));
+                res = fmaxf(res, fmaxf(row_viol(dla, r.dinv[1]), row_viol(dlb, r.dinv[2])));
             }
     };
 
@@ -1823,7 +1868,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             for (int d = 8; d >= 0; d--) limit_row(d);
         }
         contacts();
-        if (res <= kResidualAbs) break;
+        if (res <= 0.0f) break;
         PS_COUNT_IT();
         L = lds.opaque();
         res = 0.0f;
@@ -1834,7 +1879,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
 #pragma unroll
         for (int d = 0; d < 9; d++) motor_row(d);
         contacts();
-        if (res <= kResidualAbs) break;
+        if (res <= 0.0f) break;
     }
     } else {
         group_pgs<NOBJ, SHAPE, STD_MOTORS, G>(mt, Mi, lds, gate_lim, lim_up, lim_on, gate_ground[0], gate_robot,
