@@ -35,12 +35,13 @@ def contact_cache_floats(n_objects: int) -> int:
 def algorithmic_bytes_per_env_step(obs_dim: int, action_dim: int, goal_dim: int = 3, n_objects: int = 1) -> int:
     """Bytes one env-step must move through HBM:
     read q,qd (18 f32), 13 f32 per object, the contact cache, goal (f64),
-    TimeLimit counter, action; write q,qd, 45 motor f32, objects, the contact
-    cache, counter, obs, ag, dg (f32), reward, 2 flags, final_obs + final_ag.
-    PandaPush-v3: 738 B."""
+    TimeLimit counter, action; write q,qd, the 9 motor targets and 9 max
+    impulses (the gain rows are invariant, pandasim.hip store_motor_targets),
+    objects, the contact cache, counter, obs, ag, dg (f32), reward, 2 flags,
+    final_obs + final_ag.  PandaPush-v3: 630 B."""
     cache = contact_cache_floats(n_objects) * 4
     read = 18 * 4 + 13 * 4 * n_objects + cache + goal_dim * 8 + 4 + action_dim * 4
-    write = (18 * 4 + 45 * 4 + 13 * 4 * n_objects + cache + 4 + obs_dim * 4 + 2 * goal_dim * 4 + 4 + 2
+    write = (18 * 4 + 18 * 4 + 13 * 4 * n_objects + cache + 4 + obs_dim * 4 + 2 * goal_dim * 4 + 4 + 2
              + obs_dim * 4 + goal_dim * 4)
     return read + write
 

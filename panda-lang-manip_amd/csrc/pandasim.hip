@@ -135,13 +135,15 @@ PS_D void load_motors(const StateView &s, int64_t i, Motors &m) {
         m.imp[d] = s.F(PS_F_MIMP + d, i);
     }
 }
-PS_D void store_motors(const StateView &s, int64_t i, const Motors &m) {
+// The fused step writes only what it changes: every writer of the motor rows
+// (k_init_state, the plugin path's setJointMotorControlArray in sim.py, this
+// step) sets PyBullet's POSITION_CONTROL gains (kp 0.1, kd 1, target velocity
+// 0), so those three rows are invariant and the step stores the targets and
+// the max impulses only (72 B per env instead of 180 B).
+PS_D void store_motor_targets(const StateView &s, int64_t i, const Motors &m) {
 #pragma unroll
     for (int d = 0; d < 9; d++) {
         s.F(PS_F_MTARGET + d, i) = m.target[d];
-        s.F(PS_F_MKP + d, i) = m.kp[d];
-        s.F(PS_F_MKD + d, i) = m.kd[d];
-        s.F(PS_F_MVEL + d, i) = m.vel[d];
         s.F(PS_F_MIMP + d, i) = m.imp[d];
     }
 }
@@ -168,27 +170,33 @@ PS_D void store_rng(const StateView &s, int64_t i, const Pcg &r) {
 }
 PS_D uint64_t &aux_rng(const StateView &s, int64_t i) { return s.rng[4 * s.stride + i]; }
 
-// The motor rows' targets/gains are constant over a control step: they are
-// re-read from the (L2-resident) state buffer at every substep instead of
-// occupying 45 registers through the solver.  The index goes through an empty
-// asm so the loads cannot be hoisted out of the substep loop.
+// The motor rows are constant over a control step.  The fused step's targets
+// (its gains are PyBullet's defaults, STD_MOTORS) stay in 9 registers across
+// the substeps; the plugin path's full rows (45 floats) are re-read from the
+// state at every substep instead of occupying registers through the solver
+// (the index goes through an empty asm so the loads stay in the loop).
 template <int NOBJ, int SHAPE, bool STD_MOTORS, int G = 1>
 PS_D void run_substeps(const KParams &P, int64_t i, int n, float q[9], float qd[9], Body *bd,
                        const MJStore &lds, bool live PS_PROF_PARAM) {
+    static_assert(kBlock == 64, "WarmCache: one wave per workgroup");
+    const WarmCache<G, NOBJ> wc{P.s.f + PS_F_WG0 * P.s.stride, P.s.stride, live, lds};
+    wc.to_lds();
+    float tgt[9];
+#pragma unroll
+    for (int d = 0; d < 9; d++) tgt[d] = STD_MOTORS ? P.s.F(PS_F_MTARGET + d, i) : 0.0f;
     for (int st = 0; st < n; st++) {
         int64_t ii = i;
         asm volatile("" : "+v"(ii));
-        static_assert(kBlock == 64, "WarmCache: one wave per workgroup");
-        const WarmCache<G> wc{P.s.f + PS_F_WG0 * P.s.stride, P.s.stride, live};
         Motors m;
         if constexpr (STD_MOTORS) {
 #pragma unroll
-            for (int d = 0; d < 9; d++) m.target[d] = P.s.F(PS_F_MTARGET + d, ii);
+            for (int d = 0; d < 9; d++) m.target[d] = tgt[d];
         } else {
             load_motors(P.s, ii, m);
         }
         substep<NOBJ, SHAPE, STD_MOTORS, G>(P.sc, q, qd, m, bd, lds, wc PS_PROF_ARG);
     }
+    wc.from_lds();
 }
 
 // ------------------------------------------------------- task layer pieces
@@ -445,6 +453,11 @@ __global__ __launch_bounds__(kBlock) void k_init_state(KParams P) {
     if (i >= P.n) return;
     const StateView &s = P.s;
     for (int r = 0; r < PS_NUM_FLOAT_ROWS; r++) s.F(r, i) = 0.0f;
+    // POSITION_CONTROL gains (store_motor_targets); zero max impulse = no motor yet
+    for (int d = 0; d < 9; d++) {
+        s.F(PS_F_MKP + d, i) = (float)PM_MOTOR_KP;
+        s.F(PS_F_MKD + d, i) = (float)PM_MOTOR_KD;
+    }
     s.F(PS_F_CQUAT + 3, i) = 1.0f;
     s.F(PS_F_C2QUAT + 3, i) = 1.0f;
     for (int d = 0; d < 9; d++) {
@@ -514,7 +527,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
     {
         Motors m;
         set_action<CONTROL>(P, actions + i * P.action_dim, q, m);
-        if (writer) store_motors(s, i, m);
+        if (writer) store_motor_targets(s, i, m);
     }
     PS_PHASE(6);
     __shared__ float smem[lds_floats<T::NOBJ>() * kBlock];

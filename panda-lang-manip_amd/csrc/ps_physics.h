@@ -547,11 +547,18 @@ constexpr int NP = PM_MAX_PAIR_CONTACTS;
 // pose): they wait in LDS across the solve instead of holding registers.
 constexpr int LDS_STASH_OFFSET = NR * 27;
 constexpr int LDS_STASH_FLOATS = 40;
-constexpr int LDS_MI_OFFSET = LDS_STASH_OFFSET + LDS_STASH_FLOATS;
+// Then the scenes with at most one object hold their contact cache (the
+// object's ground rows and the gripper rows, 10 floats) in LDS across the
+// control step's substeps: loaded from the state once per step and written
+// back once (run_substeps), not read and written through L2 every substep.
+constexpr int LDS_CACHE_OFFSET = LDS_STASH_OFFSET + LDS_STASH_FLOATS;
+constexpr int LDS_CACHE_FLOATS = 10;
+constexpr int LDS_MI_OFFSET = LDS_CACHE_OFFSET + LDS_CACHE_FLOATS;
 #ifdef PS_MI_LDS
 constexpr int LDS_FLOATS = LDS_MI_OFFSET + 45;
 #else
 constexpr int LDS_FLOATS = LDS_MI_OFFSET;
+static_assert(LDS_FLOATS * 4 * 64 * 4 <= 160 * 1024, "four workgroups per CU");
 #endif
 // Stack (two cubes) keeps in LDS the gripper rows' J (the slots the other
 // scenes use for M^-1 J^T; the loop forms M^-1 J^T from the M^-1 registers)
@@ -606,6 +613,7 @@ struct MJStore {
     int stride;
     PS_D lds_float &at(int slot, int row, int k) const { return base[((slot * 3 + row) * 9 + k) * stride]; }
     PS_D lds_float &mi(int k) const { return base[(LDS_MI_OFFSET + k) * stride]; }
+    PS_D lds_float &cache(int k) const { return base[(LDS_CACHE_OFFSET + k) * stride]; }
     PS_D lds_float &stash(int k) const { return base[(LDS_STASH_OFFSET + k) * stride]; }
     // Stack: the stash in global memory ([GSTASH_PAIR_OFFSET][stride] floats, this env's column)
     float *gst = nullptr;
@@ -794,18 +802,49 @@ PS_D float joint_viol(float dl, float den) { return fmaf(fabsf(dl), den, -kResid
 // + lane) / G.  With G > 1 every lane of a group computes the same values;
 // lanes of a group past the batch end (live = false) compute a copy of the
 // last env and store nothing.
-template <int G>
+// Scenes with at most one object (IN_LDS) use rows WG0..WG0ID and WR..WRID
+// only, held in LDS slots 0-4 and 5-9 over the substeps (cache_to_lds,
+// cache_from_lds); Stack reads and writes the state rows directly.
+template <int G, int NOBJ>
 struct WarmCache {
+    static constexpr bool IN_LDS = NOBJ <= 1;
     float *base;  // &f[PS_F_WG0 * stride]
     int64_t stride;
     bool live;
+    MJStore lds;
+    PS_D static int slot(int row) { return row < PS_F_WG1 ? row - PS_F_WG0 : 5 + (row - PS_F_WR); }
     PS_D float &at(int row) const {
         int64_t e = ((int64_t)blockIdx.x * 64 + (int)__lane_id()) / G;
         return base[(int64_t)(row - PS_F_WG0) * stride + e];
     }
-    PS_D float load(int row) const { return at(row); }
+    PS_D float load(int row) const {
+        if constexpr (IN_LDS) return lds.cache(slot(row));
+        else return at(row);
+    }
     PS_D void store(int row, float v) const {
-        if (G == 1 || live) at(row) = v;
+        if constexpr (IN_LDS) lds.cache(slot(row)) = v;
+        else if (G == 1 || live) at(row) = v;
+    }
+    // once per control step, around the substep loop
+    PS_D void to_lds() const {
+        if constexpr (IN_LDS) {
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                lds.cache(k) = at(PS_F_WG0 + k);
+                lds.cache(5 + k) = at(PS_F_WR + k);
+            }
+        }
+    }
+    PS_D void from_lds() const {
+        if constexpr (IN_LDS) {
+            if (G == 1 || live) {
+#pragma unroll
+                for (int k = 0; k < 5; k++) {
+                    at(PS_F_WG0 + k) = lds.cache(k);
+                    at(PS_F_WR + k) = lds.cache(5 + k);
+                }
+            }
+        }
     }
 };
 // slot k's id (1 + feature, 0 = empty) of a packed id row
@@ -1008,7 +1047,7 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
 // only the targets are per-env; otherwise every gain comes from `mt`.
 template <int NOBJ, int SHAPE, bool STD_MOTORS, int G = 1>
 PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Body *bd, const MJStore &lds,
-                  const WarmCache<G> &wc PS_PROF_PARAM) {
+                  const WarmCache<G, NOBJ> &wc PS_PROF_PARAM) {
     static_assert(NOBJ >= 0 && NOBJ <= 2, "objects");
     static_assert(NOBJ < 2 || SHAPE == SHAPE_BOX, "Stack stacks cubes");
     constexpr int NB = NOBJ > 0 ? NOBJ : 1;  // array extents

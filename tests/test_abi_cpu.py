@@ -124,8 +124,8 @@ def test_bench_algorithmic_bytes_and_pmc_entries():
     import bench
 
     # + the contact cache: 10 rows read and written (ground of the cube, gripper)
-    assert bench.algorithmic_bytes_per_env_step(obs_dim=18, action_dim=3) == 738  # PandaPush-v3
-    assert bench.algorithmic_bytes_per_env_step(obs_dim=6, action_dim=3, n_objects=0) == 498  # PandaReach-v3
+    assert bench.algorithmic_bytes_per_env_step(obs_dim=18, action_dim=3) == 630  # PandaPush-v3
+    assert bench.algorithmic_bytes_per_env_step(obs_dim=6, action_dim=3, n_objects=0) == 390  # PandaReach-v3
     traffic = bench.load_pmc("PandaPush-v3 x65536/gpu")
     assert traffic is None or traffic > 0
     valu = bench.load_pmc("PandaPush-v3 x65536/gpu", "valu_insts_per_launch")

@@ -50,7 +50,7 @@ def test_bench_single_rank_roofline_blocks():
     assert out.returncode == 0, out.stderr[-3000:]
     line = _json_line(out.stdout)
     rf = line["roofline"]
-    assert rf["bound"] == "hbm" and rf["bytes_per_env_step"] == 738 and 0 < rf["frac"] < 1
+    assert rf["bound"] == "hbm" and rf["bytes_per_env_step"] == 630 and 0 < rf["frac"] < 1
     fp = rf["fp32"]
     assert fp["flops_per_env_step"] > 1e5 and 0 < fp["frac"] < 1 and fp["peak_tflops"] == 157.3
     assert set(fp["split"]) == {"dynamics_and_rows", "pgs", "ik", "step"}
