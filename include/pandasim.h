@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PS_ABI_VERSION 4
+#define PS_ABI_VERSION 5
 
 /* the six registered tasks (panda_gym/__init__.py:8-54) */
 enum {
@@ -173,6 +173,15 @@ int ps_step_lanes(const ps_ctx *ctx); /* the value ps_step uses */
  * continues, as in auto-reset) and reported truncated, even when ps_step's
  * autoreset is 0.  flags == NULL and reset_nonfinite == 0 turn it off. */
 int ps_set_nonfinite_guard(ps_ctx *ctx, uint8_t *flags, int reset_nonfinite);
+
+/* The fused step sets POSITION_CONTROL on all nine joints (panda.py:52-107 ->
+ * control_joints, pybullet.py:462-477), as env.step does.  It stores the
+ * motor targets and max impulses every step but the gain rows (kp, kd,
+ * target velocity) only when they may differ from its own: on the first
+ * ps_step after ps_create or ps_init_state, and after this call.  A caller
+ * that writes motor rows itself (the plugin path's control_joints), restores
+ * a state snapshot or passes a different state buffer calls it first. */
+int ps_mark_motor_rows_dirty(ps_ctx *ctx);
 
 /* Engine level: PyBullet.step() (pybullet.py:52-55) with the motors already in
  * the state (n_substeps of 1/500 s). */

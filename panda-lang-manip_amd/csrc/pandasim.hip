@@ -25,6 +25,7 @@ struct ps_ctx {
     uint8_t *nonfinite;   // ps_set_nonfinite_guard: per-env flag output of ps_step (caller-owned), or NULL
     int reset_nonfinite;  // ... and reset such envs in-kernel
     int lanes_per_env;    // ps_set_lanes_per_env: 0 auto, 1 or 16
+    int gains_dirty;      // the state's motor gain rows may differ from the fused step's (store_motor_gains)
 };
 
 #ifdef PS_PROFILE_PHASES
@@ -93,6 +94,7 @@ struct KParams {
     uint8_t *nonfinite;  // NaN/Inf guard output (ps_set_nonfinite_guard), NULL = off
     int reset_nonfinite;
     float *gstash;  // Stack: GSTASH_FLOATS x stride per-substep stash and pair rows (ctx scratch)
+    int write_gains;  // k_step also stores the motor gain rows (ps_ctx::gains_dirty)
 };
 
 Scene scene_of(const ps_config &c) {
@@ -135,16 +137,26 @@ PS_D void load_motors(const StateView &s, int64_t i, Motors &m) {
         m.imp[d] = s.F(PS_F_MIMP + d, i);
     }
 }
-// The fused step writes only what it changes: every writer of the motor rows
-// (k_init_state, the plugin path's setJointMotorControlArray in sim.py, this
-// step) sets PyBullet's POSITION_CONTROL gains (kp 0.1, kd 1, target velocity
-// 0), so those three rows are invariant and the step stores the targets and
-// the max impulses only (72 B per env instead of 180 B).
+// The fused step's motors are POSITION_CONTROL with PyBullet's gains (kp 0.1,
+// kd 1, target velocity 0) on all nine joints.  It stores the targets and max
+// impulses every step (72 B per env) and the three gain rows (108 B) only when
+// they may hold something else: on the first step after ps_create /
+// ps_init_state, or after ps_mark_motor_rows_dirty (the plugin path's
+// control_joints, a restored snapshot).  Until then they hold PyBullet's
+// default velocity motors (kp 0, kd 1, k_init_state).
 PS_D void store_motor_targets(const StateView &s, int64_t i, const Motors &m) {
 #pragma unroll
     for (int d = 0; d < 9; d++) {
         s.F(PS_F_MTARGET + d, i) = m.target[d];
         s.F(PS_F_MIMP + d, i) = m.imp[d];
+    }
+}
+PS_D void store_motor_gains(const StateView &s, int64_t i, const Motors &m) {
+#pragma unroll
+    for (int d = 0; d < 9; d++) {
+        s.F(PS_F_MKP + d, i) = m.kp[d];
+        s.F(PS_F_MKD + d, i) = m.kd[d];
+        s.F(PS_F_MVEL + d, i) = m.vel[d];
     }
 }
 PS_D int body_row(int b) { return b == 0 ? PS_F_CPOS : PS_F_C2POS; }
@@ -453,11 +465,6 @@ __global__ __launch_bounds__(kBlock) void k_init_state(KParams P) {
     if (i >= P.n) return;
     const StateView &s = P.s;
     for (int r = 0; r < PS_NUM_FLOAT_ROWS; r++) s.F(r, i) = 0.0f;
-    // POSITION_CONTROL gains (store_motor_targets); zero max impulse = no motor yet
-    for (int d = 0; d < 9; d++) {
-        s.F(PS_F_MKP + d, i) = (float)PM_MOTOR_KP;
-        s.F(PS_F_MKD + d, i) = (float)PM_MOTOR_KD;
-    }
     s.F(PS_F_CQUAT + 3, i) = 1.0f;
     s.F(PS_F_C2QUAT + 3, i) = 1.0f;
     for (int d = 0; d < 9; d++) {
@@ -527,7 +534,10 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
     {
         Motors m;
         set_action<CONTROL>(P, actions + i * P.action_dim, q, m);
-        if (writer) store_motor_targets(s, i, m);
+        if (writer) {
+            store_motor_targets(s, i, m);
+            if (P.write_gains) store_motor_gains(s, i, m);
+        }
     }
     PS_PHASE(6);
     __shared__ float smem[lds_floats<T::NOBJ>() * kBlock];
@@ -1157,6 +1167,7 @@ KParams params_of(ps_ctx *c, void *state) {
     P.gstash = c->gstash;
     P.nonfinite = nullptr;
     P.reset_nonfinite = 0;
+    P.write_gains = 0;
     return P;
 }
 
@@ -1252,6 +1263,7 @@ int ps_create(const ps_config *cfg, int64_t num_envs, int device, ps_ctx **out) 
     c->cfg = *cfg;
     c->num_envs = num_envs;
     c->device = device;
+    c->gains_dirty = 1;
     ps_state_layout(num_envs, &c->lay);
     *out = c;
     return PS_OK;
@@ -1281,7 +1293,14 @@ int ps_init_state(ps_ctx *c, void *state, void *stream) {
     if (!c || !state) return fail(c, PS_ERR_ARG, "null argument");
     KParams P = params_of(c, state);
     hipLaunchKernelGGL(k_init_state, grid_of(P.n, kBlock), dim3(kBlock), 0, (hipStream_t)stream, P);
+    c->gains_dirty = 1;
     return check_launch(c);
+}
+
+int ps_mark_motor_rows_dirty(ps_ctx *c) {
+    if (!c) return PS_ERR_ARG;
+    c->gains_dirty = 1;
+    return PS_OK;
 }
 
 int ps_reset(ps_ctx *c, void *state, const uint8_t *mask, const uint64_t *seeds, float *obs, float *ag, float *dg,
@@ -1323,6 +1342,7 @@ int ps_step(ps_ctx *c, void *state, const float *actions, float *obs, float *ag,
     P.autoreset = autoreset;
     P.nonfinite = c->nonfinite;
     P.reset_nonfinite = c->reset_nonfinite;
+    P.write_gains = c->gains_dirty;
     const int lanes = ps_step_lanes(c);
     dim3 g = grid_of(P.n * lanes, kBlock), b(kBlock);
     hipStream_t st = (hipStream_t)stream;
@@ -1354,7 +1374,9 @@ int ps_step(ps_ctx *c, void *state, const float *actions, float *obs, float *ag,
     }
 #undef PS_LAUNCH_TASK
 #undef PS_LAUNCH_STEP
-    return check_launch(c);
+    const int rc = check_launch(c);
+    if (rc == PS_OK) c->gains_dirty = 0;
+    return rc;
 }
 
 int ps_set_lanes_per_env(ps_ctx *c, int lanes) {

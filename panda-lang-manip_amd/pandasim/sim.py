@@ -497,6 +497,7 @@ class PandaSim:
         if state_id not in self._saved:
             raise L.PandasimError(f"restoreState: unknown state id {state_id}")
         self.state.copy_(self._saved[state_id])
+        self._call("ps_mark_motor_rows_dirty", self._ctx)  # the snapshot's motor rows
 
     def remove_state(self, state_id: int) -> None:
         """pybullet.py:274-280."""
@@ -632,6 +633,7 @@ class PandaSim:
             self.f[L.F_MKD + d, :self.num_envs] = 1.0
             self.f[L.F_MVEL + d, :self.num_envs] = 0.0
             self.f[L.F_MIMP + d, :self.num_envs] = float(forces[k]) * DT_SUBSTEP
+        self._call("ps_mark_motor_rows_dirty", self._ctx)  # a fused step rewrites the gains
 
     def inverse_kinematics(self, body: str, link: int, position, orientation) -> torch.Tensor:
         """calculateInverseKinematics from the current joints (pybullet.py:479-497) -> [B, 9]."""

@@ -90,3 +90,33 @@ def test_group_kernel_shards_bit_identical():
         parts = [e.step(acts[k][r * (B // W):(r + 1) * (B // W)])[0] for r, e in enumerate(shards)]
         for key in of:
             assert torch.equal(of[key], torch.cat([p[key] for p in parts])), (k, key)
+
+
+def test_motor_gain_rows_follow_the_fused_step():
+    """env.step sets POSITION_CONTROL with PyBullet's gains on all nine joints
+    (panda.py:52-107, pybullet.py:462-477).  The fused step writes the gain rows
+    only when they may differ (ps_mark_motor_rows_dirty): a fresh state's
+    default velocity motors, and after the plugin path's control_joints."""
+    import pandasim
+    from pandasim import _lib as L
+
+    B = 8
+    env = pandasim.make("PandaPush-v3", num_envs=B)
+    env.reset(seed=3)
+    f = env.sim.f
+    assert torch.all(f[L.F_MKP:L.F_MKP + 9, :B] == 0.0)  # k_init_state: default velocity motors
+    a = torch.zeros(B, env.action_dim, device="cuda")
+    env.step(a)
+
+    def gains():
+        return f[L.F_MKP:L.F_MVEL + 9, :B].clone(), f[L.F_MIMP:L.F_MIMP + 9, :B].clone()
+
+    kp_kd_vel, imp = gains()
+    assert torch.allclose(kp_kd_vel[:9], torch.full_like(kp_kd_vel[:9], 0.1))
+    assert torch.all(kp_kd_vel[9:18] == 1.0) and torch.all(kp_kd_vel[18:] == 0.0)
+    # the plugin path changes joint 5's motor; the next fused step restores all nine
+    env.sim.control_joints("panda", [5], [0.3], [5.0])
+    f[L.F_MKD + 5, :B] = 0.5  # a gain no writer of the fused path uses
+    env.step(a)
+    kp_kd_vel2, imp2 = gains()
+    assert torch.equal(kp_kd_vel2, kp_kd_vel) and torch.equal(imp2, imp)
