@@ -218,7 +218,7 @@ def main():
     ap.add_argument("--batch", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--lanes", type=int, default=0, help="lanes per env of the step kernel: 1, 16, 0 = auto")
+    ap.add_argument("--lanes", type=int, default=0, help="lanes per env of the step kernel: 1, 8, 16, 0 = auto")
     args = ap.parse_args()
 
     import torch

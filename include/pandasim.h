@@ -155,13 +155,14 @@ int ps_step(ps_ctx *ctx, void *state, const float *actions, float *obs, float *a
             void *stream);
 
 /* Lanes per env of ps_step's kernel: 1 (one env per lane, the large-batch
- * kernel) or 16 (a group of 16 lanes shares each env's constraint solve --
- * the small-batch kernel, one object at most: not Stack); 0 (default) picks
- * 16 for batches of at most PS_GROUP_AUTO_MAX_ENVS envs and 1 above.  The two
- * kernels sum in different orders, so their results agree to fp32 rounding,
- * not bit for bit: fix the value to compare runs of different batch sizes
- * bit for bit. */
-#define PS_GROUP_AUTO_MAX_ENVS 4096
+ * kernel), 16 or 8 (a group of 16 or 8 lanes shares each env's constraint
+ * solve -- the small-batch kernels, one object at most: not Stack); 0
+ * (default) picks 16 for batches of at most PS_GROUP16_AUTO_MAX_ENVS envs, 8
+ * up to PS_GROUP8_AUTO_MAX_ENVS and 1 above.  The kernels sum in different
+ * orders, so their results agree to fp32 rounding, not bit for bit: fix the
+ * value to compare runs of different batch sizes bit for bit. */
+#define PS_GROUP16_AUTO_MAX_ENVS 4096
+#define PS_GROUP8_AUTO_MAX_ENVS 8192
 int ps_set_lanes_per_env(ps_ctx *ctx, int lanes);
 int ps_step_lanes(const ps_ctx *ctx); /* the value ps_step uses */
 

@@ -1356,6 +1356,11 @@ int ps_step(ps_ctx *c, void *state, const float *actions, float *obs, float *ag,
                                        terminated, truncated, final_obs, final_ag);                              \
                     break;                                                                                       \
                 }                                                                                                \
+                if (lanes == 8) {                                                                                \
+                    hipLaunchKernelGGL((k_step<T, C, 8>), g, b, 0, st, P, actions, obs, ag, dg, reward,          \
+                                       terminated, truncated, final_obs, final_ag);                              \
+                    break;                                                                                       \
+                }                                                                                                \
             }                                                                                                    \
             hipLaunchKernelGGL((k_step<T, C>), g, b, 0, st, P, actions, obs, ag, dg, reward, terminated,        \
                                truncated, final_obs, final_ag);                                                  \
@@ -1380,8 +1385,8 @@ int ps_step(ps_ctx *c, void *state, const float *actions, float *obs, float *ag,
 }
 
 int ps_set_lanes_per_env(ps_ctx *c, int lanes) {
-    if (!c || !(lanes == 0 || lanes == 1 || lanes == 16)) return PS_ERR_ARG;
-    if (lanes == 16 && c->cfg.n_objects > 1) return fail(c, PS_ERR_UNSUPPORTED, "16 lanes per env: one object at most");
+    if (!c || !(lanes == 0 || lanes == 1 || lanes == 8 || lanes == 16)) return PS_ERR_ARG;
+    if (lanes > 1 && c->cfg.n_objects > 1) return fail(c, PS_ERR_UNSUPPORTED, "8 or 16 lanes per env: one object at most");
     c->lanes_per_env = lanes;
     return PS_OK;
 }
@@ -1389,7 +1394,9 @@ int ps_set_lanes_per_env(ps_ctx *c, int lanes) {
 int ps_step_lanes(const ps_ctx *c) {
     if (!c) return PS_ERR_ARG;
     if (c->lanes_per_env) return c->lanes_per_env;
-    return c->cfg.n_objects <= 1 && c->num_envs <= PS_GROUP_AUTO_MAX_ENVS ? 16 : 1;
+    if (c->cfg.n_objects > 1) return 1;
+    if (c->num_envs <= PS_GROUP16_AUTO_MAX_ENVS) return 16;
+    return c->num_envs <= PS_GROUP8_AUTO_MAX_ENVS ? 8 : 1;
 }
 
 int ps_set_nonfinite_guard(ps_ctx *c, uint8_t *flags, int reset_nonfinite) {

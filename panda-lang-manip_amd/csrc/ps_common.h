@@ -247,6 +247,26 @@ PS_D float group16_bcast(float x) {
     return dpp_f<0x150 + K>(x);
 }
 
+// the same over groups of 8 lanes: half_mirror pairs lane i with 7 - i, then
+// the quad swaps (every lane of the group ends with the same bits)
+PS_D float group8_sum(float x) {
+    x += dpp_f<0x141>(x);  // row_half_mirror
+    x += dpp_f<0xB1>(x);   // quad_perm [1,0,3,2]
+    x += dpp_f<0x4E>(x);   // quad_perm [2,3,0,1]
+    return x;
+}
+
+// lane K of this lane's 8-lane group, in every lane of the group: lane K % 4
+// of each quad (quad_perm), and the other quad's value through half_mirror
+template <int K>
+PS_D float group8_bcast(float x) {
+    static_assert(K >= 0 && K < 8, "lane of the group");
+    constexpr int q = K & 3;
+    const float y = dpp_f<q | (q << 2) | (q << 4) | (q << 6)>(x);
+    const float z = dpp_f<0x141>(y);
+    return ((__lane_id() & 4u) == (unsigned)(K & 4)) ? y : z;
+}
+
 // compile-time loop
 template <int B, int E, typename F>
 PS_D void static_for(F &&f) {

@@ -865,99 +865,132 @@ PS_D float cone_scale(float m2, float lim) {
     return m2 > lim * lim ? lim * __builtin_amdgcn_rsqf(fmaxf(m2, 1.17549435e-38f)) : 1.0f;
 }
 
-// Projected Gauss-Seidel with G = 16 lanes per env (the small-batch step
-// kernel): every lane of a group ran the same setup, lane e
-// owns velocity DoF e (robot DoFs 0-8, then the object's omega 9-11 and
-// v 12-14) and keeps its slice of every row's J and M^-1 J^T.  A row is then
-// one product per lane, a 16-lane sum (group16_sum: the same bits in every
-// lane, so every lane computes the same impulse), the clamp, and one FMA per
-// lane -- about 11 instructions for a row the one-lane solver spends 20-60
-// on.  Row order, gates, bounds and the stopping rule are the one-lane
-// solver's.  Returns the full velocity change in every lane of the group.
+// Projected Gauss-Seidel with G = 16 or 8 lanes per env (the small-batch
+// step kernels): every lane of a group ran the same setup, and
+// the 15 velocity DoFs (robot 0-8, then the object's omega 9-11 and v 12-14)
+// are dealt to the lanes: lane e owns DoFs e + k G for k < 16 / G (G = 16: one
+// DoF per lane; G = 8: two) with their slices of every row's J and M^-1 J^T.
+// A row is then one product per owned DoF, a group sum (group_sum: the same
+// bits in every lane, so every lane computes the same impulse), the clamp,
+// and one FMA per owned DoF -- about 11 instructions for a row the one-lane
+// solver spends 20-60 on.  Row order, gates, bounds and the stopping rule are
+// the one-lane solver's.  Returns the full velocity change in every lane.
+template <int G>
+PS_D float group_sum(float x) {
+    if constexpr (G == 16) return group16_sum(x);
+    else return group8_sum(x);
+}
+template <int G, int K>
+PS_D float group_bcast(float x) {
+    if constexpr (G == 16) return group16_bcast<K>(x);
+    else return group8_bcast<K>(x);
+}
 template <int NOBJ, int SHAPE, bool STD_MOTORS, int G>
 PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, unsigned gate_lim, unsigned lim_up,
                     unsigned lim_on, unsigned gate_gnd, unsigned gate_robot, const float dinvj[9],
                     const float lim_rhs[9], float lim_lam[9], const float mot_rhs[9], float mot_lam[9],
                     GroundContact gc[NG], RobotContact rc[NR], const BodyDyn<SHAPE> &od, float gmu, float dv[9],
                     V3 &dw, V3 &dvl PS_PROF_COUNT_PARAM) {
-    static_assert(G == 16 && NOBJ <= 1, "groups of 16 lanes hold 9 robot + 6 object DoFs");
-    const int e = (int)(__lane_id() & 15u);
-    // lane e's slices: row e of M^-1 (joint rows), object-only rows, robot rows
-    float mrow[9], midg[9];
+    static_assert((G == 16 || G == 8) && NOBJ <= 1, "groups of 16 or 8 lanes hold 9 robot + 6 object DoFs");
+    constexpr int K = 16 / G;  // DoFs per lane
+    const int e = (int)(__lane_id() & (unsigned)(G - 1));
+    // lane e's slices: rows e + k G of M^-1 (joint rows), object-only rows, robot rows
+    float mrow[K][9], midg[9];
 #pragma unroll
     for (int d = 0; d < 9; d++) {
-        float v = 0.0f;
 #pragma unroll
-        for (int k = 0; k < 9; k++) v = e == k ? Mi[sidx(k, d)] : v;
-        mrow[d] = v;
+        for (int k = 0; k < K; k++) {
+            float v = 0.0f;
+#pragma unroll
+            for (int r = 0; r < 9; r++) v = e + k * G == r ? Mi[sidx(r, d)] : v;
+            mrow[k][d] = v;
+        }
         midg[d] = Mi[sidx(d, d)];
     }
-    auto oslice = [&](V3 a, V3 l) {
+    auto oslice = [&](int k, V3 a, V3 l) {
+        const int dof = e + k * G;
         float v = 0.0f;
-        v = e == 9 ? a.x : v;
-        v = e == 10 ? a.y : v;
-        v = e == 11 ? a.z : v;
-        v = e == 12 ? l.x : v;
-        v = e == 13 ? l.y : v;
-        v = e == 14 ? l.z : v;
+        v = dof == 9 ? a.x : v;
+        v = dof == 10 ? a.y : v;
+        v = dof == 11 ? a.z : v;
+        v = dof == 12 ? l.x : v;
+        v = dof == 13 ? l.y : v;
+        v = dof == 14 ? l.z : v;
         return v;
     };
-    float gJ[NG][3], gM[NG][3];
+    float gJ[NG][3][K], gM[NG][3][K];
 #pragma unroll
     for (int c = 0; c < NG; c++)
 #pragma unroll
-        for (int j = 0; j < 3; j++) {
-            gJ[c][j] = gM[c][j] = 0.0f;
-            if constexpr (NOBJ > 0) {
-                V3 dir = j == 0 ? mk(0, 0, 1) : (j == 1 ? mk(0, -1, 0) : mk(1, 0, 0));
-                V3 rn = cross(gc[c].r, dir);
-                gJ[c][j] = oslice(rn, dir);
-                gM[c][j] = oslice(od.inv_inertia(rn), dir * od.inv_m);
+        for (int j = 0; j < 3; j++)
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                gJ[c][j][k] = gM[c][j][k] = 0.0f;
+                if constexpr (NOBJ > 0) {
+                    V3 dir = j == 0 ? mk(0, 0, 1) : (j == 1 ? mk(0, -1, 0) : mk(1, 0, 0));
+                    V3 rn = cross(gc[c].r, dir);
+                    gJ[c][j][k] = oslice(k, rn, dir);
+                    gM[c][j][k] = oslice(k, od.inv_inertia(rn), dir * od.inv_m);
+                }
             }
-        }
-    float rJ[NR][3], rM[NR][3];
+    float rJ[NR][3][K], rM[NR][3][K];
     {
         const MJStore W = lds.opaque();
-        const int ke = e < 9 ? e : 8;
 #pragma unroll
         for (int c = 0; c < NR; c++)
 #pragma unroll
-            for (int j = 0; j < 3; j++) {
-                float v = 0.0f;
+            for (int j = 0; j < 3; j++)
 #pragma unroll
-                for (int k = 0; k < 9; k++) v = e == k ? rc[c].J[j][k] : v;
-                float m = (float)W.at(c, j, ke);
-                m = e < 9 ? m : 0.0f;
-                if constexpr (NOBJ > 0) {
-                    // the object is body B: -rn, -dir
-                    V3 rn = rc[c].rn[j], dir = rc[c].dir[j];
-                    v += oslice(mk(-rn.x, -rn.y, -rn.z), mk(-dir.x, -dir.y, -dir.z));
-                    m += oslice(od.inv_inertia(mk(-rn.x, -rn.y, -rn.z)), dir * -od.inv_m);
+                for (int k = 0; k < K; k++) {
+                    const int dof = e + k * G;
+                    float v = 0.0f;
+#pragma unroll
+                    for (int r = 0; r < 9; r++) v = dof == r ? rc[c].J[j][r] : v;
+                    float m = (float)W.at(c, j, dof < 9 ? dof : 8);
+                    m = dof < 9 ? m : 0.0f;
+                    if constexpr (NOBJ > 0) {
+                        // the object is body B: -rn, -dir
+                        V3 rn = rc[c].rn[j], dir = rc[c].dir[j];
+                        v += oslice(k, mk(-rn.x, -rn.y, -rn.z), mk(-dir.x, -dir.y, -dir.z));
+                        m += oslice(k, od.inv_inertia(mk(-rn.x, -rn.y, -rn.z)), dir * -od.inv_m);
+                    }
+                    rJ[c][j][k] = v;
+                    rM[c][j][k] = m;
                 }
-                rJ[c][j] = v;
-                rM[c][j] = m;
-            }
     }
-    float dvm = 0.0f;  // this lane's velocity change
+    float dvm[K];  // this lane's velocity changes (DoFs e + k G)
+#pragma unroll
+    for (int k = 0; k < K; k++) dvm[k] = 0.0f;
+    auto prod = [&](const float J[K]) {
+        float p = J[0] * dvm[0];
+#pragma unroll
+        for (int k = 1; k < K; k++) p = fmaf(J[k], dvm[k], p);
+        return p;
+    };
+    auto apply = [&](const float M[K], float dl) {
+#pragma unroll
+        for (int k = 0; k < K; k++) dvm[k] = fmaf(M[k], dl, dvm[k]);
+    };
     // warm start (see the one-lane solver)
 #pragma unroll
     for (int c = 0; c < NG; c++)
-        if (NOBJ > 0 && (gate_gnd & (1u << c))) dvm = fmaf(gM[c][0], gc[c].lam[0], dvm);
+        if (NOBJ > 0 && (gate_gnd & (1u << c))) apply(gM[c][0], gc[c].lam[0]);
 #pragma unroll
     for (int c = 0; c < NR; c++)
-        if (gate_robot & (1u << c)) dvm = fmaf(rM[c][0], rc[c].lam[0], dvm);
+        if (gate_robot & (1u << c)) apply(rM[c][0], rc[c].lam[0]);
 
     float res = 0.0f;
-    // a joint row's J is e_d: its product is lane d's velocity change, one
-    // DPP broadcast instead of a sum
+    // a joint row's J is e_d: its product is the velocity change of DoF d,
+    // held by lane d % G in slot d / G: one broadcast instead of a sum
     auto jrow = [&](auto DD, float sgn, float rhs, float &lam, float lo, float hi) {
         constexpr int d = decltype(DD)::value;
-        float s = group16_bcast<d>(dvm);
+        float s = group_bcast<G, d % G>(dvm[d / G]);
         float dl = rhs - dinvj[d] * (sgn * s);
         float nl = fminf(fmaxf(lam + dl, lo), hi);
         dl = nl - lam;
         lam = nl;
-        dvm = fmaf(mrow[d], sgn * dl, dvm);
+#pragma unroll
+        for (int k = 0; k < K; k++) dvm[k] = fmaf(mrow[k][d], sgn * dl, dvm[k]);
         res = fmaxf(res, joint_viol(dl, midg[d]));
     };
     auto limit_row = [&](auto DD) {
@@ -974,20 +1007,20 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         jrow(DD, 1.0f, mot_rhs[d], mot_lam[d], -imp, imp);
     };
     // rows d = 8..0 and 0..8 with compile-time d
-    auto down = [&](auto row) { static_for<0, 9>([&](auto K) { row(std::integral_constant<int, 8 - decltype(K)::value>{}); }); };
-    auto up = [&](auto row) { static_for<0, 9>([&](auto K) { row(K); }); };
-    auto normal = [&](float Jm, float Mm, float rhs, float dinv, float &lam) {
-        float s = group16_sum(Jm * dvm);
+    auto down = [&](auto row) { static_for<0, 9>([&](auto I) { row(std::integral_constant<int, 8 - decltype(I)::value>{}); }); };
+    auto up = [&](auto row) { static_for<0, 9>([&](auto I) { row(I); }); };
+    auto normal = [&](const float Jm[K], const float Mm[K], float rhs, float dinv, float &lam) {
+        float s = group_sum<G>(prod(Jm));
         float dl = rhs - dinv * s;
         float nl = fminf(fmaxf(lam + dl, 0.0f), (float)PM_CONTACT_UPPER);
         dl = nl - lam;
         lam = nl;
-        dvm = fmaf(Mm, dl, dvm);
+        apply(Mm, dl);
         res = fmaxf(res, row_viol(dl, dinv));
     };
-    auto cone = [&](const float J[3], const float M[3], const float rhs[3], const float dinv[3], float lam[3],
+    auto cone = [&](const float J[3][K], const float M[3][K], const float rhs[3], const float dinv[3], float lam[3],
                     float mu) {
-        float sa = group16_sum(J[1] * dvm), sb = group16_sum(J[2] * dvm);
+        float sa = group_sum<G>(prod(J[1])), sb = group_sum<G>(prod(J[2]));
         float dla = rhs[1] - dinv[1] * sa, dlb = rhs[2] - dinv[2] * sb;
         float a = lam[1] + dla, b = lam[2] + dlb;
         float lim = mu * fmaxf(lam[0], 0.0f);
@@ -998,13 +1031,15 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         dlb = b - lam[2];
         lam[1] = a;
         lam[2] = b;
-        dvm = fmaf(M[2], dlb, fmaf(M[1], dla, dvm));
+#pragma unroll
+        for (int k = 0; k < K; k++) dvm[k] = fmaf(M[2][k], dlb, fmaf(M[1][k], dla, dvm[k]));
         res = fmaxf(res, fmaxf(row_viol(dla, dinv[1]), row_viol(dlb, dinv[2])));
     };
     auto contacts = [&]() {
 #pragma unroll
         for (int c = 0; c < NG; c++)
-            if (NOBJ > 0 && (gate_gnd & (1u << c))) normal(gJ[c][0], gM[c][0], gc[c].rhs[0], gc[c].dinv[0], gc[c].lam[0]);
+            if (NOBJ > 0 && (gate_gnd & (1u << c)))
+                normal(gJ[c][0], gM[c][0], gc[c].rhs[0], gc[c].dinv[0], gc[c].lam[0]);
 #pragma unroll
         for (int c = 0; c < NR; c++)
             if (gate_robot & (1u << c)) normal(rJ[c][0], rM[c][0], rc[c].rhs[0], rc[c].dinv[0], rc[c].lam[0]);
@@ -1034,11 +1069,18 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         if (res <= 0.0f) break;
     }
     // every lane of the group gets the whole velocity change
-#pragma unroll
-    for (int d = 0; d < 9; d++) dv[d] = __shfl(dvm, d, G);
+    static_for<0, 9>([&](auto DD) {
+        constexpr int d = decltype(DD)::value;
+        dv[d] = __shfl(dvm[d / G], d % G, G);
+    });
     if constexpr (NOBJ > 0) {
-        dw = mk(__shfl(dvm, 9, G), __shfl(dvm, 10, G), __shfl(dvm, 11, G));
-        dvl = mk(__shfl(dvm, 12, G), __shfl(dvm, 13, G), __shfl(dvm, 14, G));
+        float o[6];
+        static_for<0, 6>([&](auto JJ) {
+            constexpr int dof = 9 + decltype(JJ)::value;
+            o[dof - 9] = __shfl(dvm[dof / G], dof % G, G);
+        });
+        dw = mk(o[0], o[1], o[2]);
+        dvl = mk(o[3], o[4], o[5]);
     }
 }
 

@@ -46,7 +46,7 @@ class PandaVecEnv:
                  device="cuda", autoreset: bool = True, lanes_per_env: int = 0):
         self.task_name, self.reward_type, self.control_type = task, reward_type, control_type
         self.sim = PandaSim(task, control_type, reward_type, num_envs, device)
-        # 0: the library picks 16 lanes per env for small batches, 1 above (ps_set_lanes_per_env)
+        # 0: the library picks 16 or 8 lanes per env for small batches, 1 above (ps_set_lanes_per_env)
         self.sim._call("ps_set_lanes_per_env", self.sim._ctx, int(lanes_per_env))
         self.lanes_per_env = self.sim._lib.ps_step_lanes(self.sim._ctx)
         self.num_envs = self.sim.num_envs

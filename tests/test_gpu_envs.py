@@ -68,9 +68,10 @@ def test_sharded_batch_matches_unsplit_batch(env_id):
             assert torch.equal(of[key], joined), (env_id, k, key)
 
 
-def test_group_kernel_shards_bit_identical():
-    """The 16-lane kernel is batch-size independent too: 4 shards of 24 envs
-    step bit for bit like the 96-env batch (the ragged last wave included)."""
+@pytest.mark.parametrize("lanes", [16, 8])
+def test_group_kernel_shards_bit_identical(lanes):
+    """The 16- and 8-lane kernels are batch-size independent too: 4 shards of
+    24 envs step bit for bit like the 96-env batch (ragged last waves included)."""
     import pandasim
     from pandasim.dist import shard_seeds
 
@@ -78,11 +79,11 @@ def test_group_kernel_shards_bit_identical():
     g = torch.Generator(device="cuda")
     g.manual_seed(9)
     acts = torch.rand(5, B, 4, device="cuda", generator=g) * 2 - 1
-    full = pandasim.make("PandaPickAndPlace-v3", num_envs=B, lanes_per_env=16)
+    full = pandasim.make("PandaPickAndPlace-v3", num_envs=B, lanes_per_env=lanes)
     full.reset(seed=shard_seeds(77, B, 1, 0).numpy().astype("uint64"))
     shards = []
     for r in range(W):
-        e = pandasim.make("PandaPickAndPlace-v3", num_envs=B // W, lanes_per_env=16)
+        e = pandasim.make("PandaPickAndPlace-v3", num_envs=B // W, lanes_per_env=lanes)
         e.reset(seed=shard_seeds(77, B, W, r).numpy().astype("uint64"))
         shards.append(e)
     for k in range(5):

@@ -42,9 +42,9 @@ def make_env(ps, task, control, n, reward="sparse", lanes=0):
     return PandaVecEnv(task, reward, control, n, "cuda", lanes_per_env=lanes)
 
 
-# ps_step kernels: one env per lane, and groups of 16 lanes per env (not Stack)
-LANES = [1, 16]
-TASKS_LANES = [(t, c, l) for t, c in TASKS for l in LANES if not (t == "stack" and l == 16)]
+# ps_step kernels: one env per lane, and groups of 16 or 8 lanes per env (not Stack)
+LANES = [1, 16, 8]
+TASKS_LANES = [(t, c, l) for t, c in TASKS for l in LANES if not (t == "stack" and l > 1)]
 
 
 # ------------------------------------------------------------ known answers
@@ -562,11 +562,12 @@ def test_gripper_object_contact_parity(ps, task):
     assert e_obj.max() < 2e-2 and e_q.max() < SIM_LOOSE["q"] * 5
 
 
-@pytest.mark.parametrize("B,lanes", [(1, 1), (70, 1), (1, 16), (7, 16), (70, 16)])
+@pytest.mark.parametrize("B,lanes", [(1, 1), (70, 1), (1, 16), (7, 16), (70, 16), (1, 8), (13, 8), (70, 8)])
 def test_ragged_batch_parity(ps, B, lanes):
     """Batches that are not a multiple of the wave (one env; 70 = a full
     64-lane wave plus 6 lanes; with 16 lanes per env, 7 envs = a wave of 4
-    plus 3 envs and a dummy group): every env, including the ragged wave's,
+    plus 3 envs and a dummy group; with 8, 13 envs = a wave of 8 plus 5 and
+    three dummy groups): every env, including the ragged wave's,
     steps like the oracle from the same state."""
     env = make_env(ps, "push", "ee", B, lanes=lanes)
     env.autoreset = False
