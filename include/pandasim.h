@@ -47,6 +47,11 @@ enum { PS_SHAPE_BOX = 0, PS_SHAPE_CYLINDER = 1 };
 #define PS_VISUAL_SPHERE 2 /* ps_visual.target_shape only: create_sphere ghost (reach.py:31-38) */
 enum { PS_OK = 0, PS_ERR_ARG = -1, PS_ERR_HIP = -2, PS_ERR_UNSUPPORTED = -3 };
 
+/* Largest batch one context holds (2^28 envs, ~260 GB of state): the kernels
+ * address an env's state rows by a 32-bit byte offset.  ps_state_layout and
+ * ps_create return PS_ERR_ARG above it. */
+#define PS_MAX_ENVS (1LL << 28)
+
 /* Scene/env configuration.  ps_default_config() fills the registered env
  * (panda_gym/__init__.py:8-54 + envs/panda_tasks.py:14-113 + the task's
  * _create_scene); the scene fields let tests build the reference's

@@ -71,8 +71,35 @@ struct StateView {
     uint64_t *rng;
     int32_t *elapsed;
     int64_t stride;
-    PS_D float &F(int row, int64_t i) const { return f[row * stride + i]; }
-    PS_D double &G(int k, int64_t i) const { return goal[k * stride + i]; }
+    // Row r of env i = a wave-uniform row base (SGPRs, rebuilt from the kernel
+    // arguments by two scalar ops) plus the lane's 32-bit byte offset, which
+    // the loads and stores take as `global_* v_off, s[base]`.  With a 64-bit
+    // per-lane address per row the compiler kept 26 of them live from the
+    // state loads at entry to the stores at exit: 208 B per lane of scratch
+    // (spilled and written back to HBM every step) and AGPR copies through the
+    // solver.  ps_create caps num_envs at PS_MAX_ENVS so i * 8 fits 32 bits.
+    // The row base goes through an empty asm pinned to SGPRs: otherwise the
+    // compiler reassociates (f + off) + row * stride back into one 64-bit
+    // per-lane pointer per row.
+    PS_D static uint32_t off(int64_t i, uint32_t size) { return (uint32_t)i * size; }
+    // (readfirstlane first: the group kernels' divergence analysis does not
+    // always see the base as uniform, and an SGPR operand needs one)
+    template <class T>
+    PS_D static T *pin(T *p) {
+        const uint64_t u = (uint64_t)p;
+        uint64_t r = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(u >> 32)) << 32) |
+                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)u);
+        asm("" : "+s"(r));
+        return (T *)r;
+    }
+    template <class T>
+    PS_D static T &at(T *row_base, int64_t i) {
+        return *(T *)((char *)pin(row_base) + off(i, sizeof(T)));
+    }
+    PS_D float &F(int row, int64_t i) const { return at(f + row * stride, i); }
+    PS_D double &G(int k, int64_t i) const { return at(goal + k * stride, i); }
+    PS_D uint64_t &R(int k, int64_t i) const { return at(rng + k * stride, i); }
+    PS_D int32_t &E(int64_t i) const { return at(elapsed, i); }
 };
 
 StateView view_of(const ps_ctx *c, void *state) {
@@ -175,12 +202,12 @@ PS_D void store_body(const StateView &s, int64_t i, int b, const Body &c) {
     s.F(r + 10, i) = c.omg.x; s.F(r + 11, i) = c.omg.y; s.F(r + 12, i) = c.omg.z;
 }
 PS_D Pcg load_rng(const StateView &s, int64_t i) {
-    return Pcg{s.rng[i], s.rng[s.stride + i], s.rng[2 * s.stride + i], s.rng[3 * s.stride + i]};
+    return Pcg{s.R(0, i), s.R(1, i), s.R(2, i), s.R(3, i)};
 }
 PS_D void store_rng(const StateView &s, int64_t i, const Pcg &r) {
-    s.rng[i] = r.sh; s.rng[s.stride + i] = r.sl; s.rng[2 * s.stride + i] = r.ih; s.rng[3 * s.stride + i] = r.il;
+    s.R(0, i) = r.sh; s.R(1, i) = r.sl; s.R(2, i) = r.ih; s.R(3, i) = r.il;
 }
-PS_D uint64_t &aux_rng(const StateView &s, int64_t i) { return s.rng[4 * s.stride + i]; }
+PS_D uint64_t &aux_rng(const StateView &s, int64_t i) { return s.R(4, i); }
 
 // The motor rows are constant over a control step.  The fused step's targets
 // (its gains are PyBullet's defaults, STD_MOTORS) stay in 9 registers across
@@ -474,7 +501,7 @@ __global__ __launch_bounds__(kBlock) void k_init_state(KParams P) {
     for (int d = 0; d < PS_MAX_GOAL_DIM; d++) s.G(d, i) = 0.0;
     store_rng(s, i, pcg_seed(0));
     aux_rng(s, i) = aux_seed(0);
-    s.elapsed[i] = 0;
+    s.E(i) = 0;
 }
 
 template <int TASK>
@@ -499,7 +526,7 @@ __global__ __launch_bounds__(kBlock) void k_reset(KParams P, const uint8_t *mask
     for (int d = 0; d < T::GOAL; d++) s.G(d, i) = g[d];
     store_rng(s, i, r);
     aux_rng(s, i) = aux;
-    s.elapsed[i] = 0;
+    s.E(i) = 0;
     clear_contact_cache(s, i);
     write_obs<TASK>(P, i, q, qd, bd, g, obs, ag, dg);
 }
@@ -543,8 +570,9 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
     __shared__ float smem[lds_floats<T::NOBJ>() * kBlock];
     MJStore lds{(lds_float *)(smem + threadIdx.x), kBlock};
     if constexpr (T::NOBJ == 2) {
-        lds.gst = P.gstash + i;
+        lds.gst = P.gstash;
         lds.gst_stride = s.stride;
+        lds.goff = StateView::off(i, 4);
         lds.gpair = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_PAIR_OFFSET * s.stride +
                                                                  i * (NP * PAIR_FLOATS));
     }
@@ -556,7 +584,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
     achieved<TASK>(P, q, qd, bd, a);
     double dist = goal_metric<TASK>(a, g);
     bool term = dist < T::THRESHOLD;
-    int el = s.elapsed[i] + 1;
+    int el = s.E(i) + 1;
     bool trunc = el >= T::STEPS;
     if (writer) {
         reward[i] = reward_for(P.reward_type, dist, T::THRESHOLD);
@@ -598,7 +626,7 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
         write_obs<TASK>(P, i, q, qd, bd, g, final_obs, final_ag, nullptr);
     }
     if (writer) {
-        s.elapsed[i] = el;
+        s.E(i) = el;
         store_robot(s, i, q, qd);
 #pragma unroll
         for (int b = 0; b < T::NOBJ; b++) store_body(s, i, b, bd[b]);
@@ -625,8 +653,9 @@ __global__ __launch_bounds__(kBlock) void k_sim_step(KParams P, int n_substeps) 
     __shared__ float smem[lds_floats<NOBJ>() * kBlock];
     MJStore lds{(lds_float *)(smem + threadIdx.x), kBlock};
     if constexpr (NOBJ == 2) {
-        lds.gst = P.gstash + i;
+        lds.gst = P.gstash;
         lds.gst_stride = s.stride;
+        lds.goff = StateView::off(i, 4);
         lds.gpair = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_PAIR_OFFSET * s.stride +
                                                                  i * (NP * PAIR_FLOATS));
     }
@@ -1230,7 +1259,7 @@ int ps_default_config(int task, int control, int reward, ps_config *out) {
 }
 
 int ps_state_layout(int64_t num_envs, ps_layout *out) {
-    if (!out || num_envs <= 0) return PS_ERR_ARG;
+    if (!out || num_envs <= 0 || num_envs > PS_MAX_ENVS) return PS_ERR_ARG;
     int64_t stride = (num_envs + 63) & ~(int64_t)63;
     out->num_envs = num_envs;
     out->stride = stride;
@@ -1243,7 +1272,7 @@ int ps_state_layout(int64_t num_envs, ps_layout *out) {
 }
 
 int ps_create(const ps_config *cfg, int64_t num_envs, int device, ps_ctx **out) {
-    if (!cfg || !out || num_envs <= 0) return PS_ERR_ARG;
+    if (!cfg || !out || num_envs <= 0 || num_envs > PS_MAX_ENVS) return PS_ERR_ARG;
     if (cfg->task < 0 || cfg->task >= PS_NUM_TASKS || cfg->control < 0 || cfg->control > 1 || cfg->reward < 0 ||
         cfg->reward > 1 || cfg->n_objects < 0 || cfg->n_objects > 2 || cfg->object_shape < 0 || cfg->object_shape > 1)
         return PS_ERR_ARG;

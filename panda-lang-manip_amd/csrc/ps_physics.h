@@ -616,12 +616,18 @@ struct MJStore {
     PS_D lds_float &cache(int k) const { return base[(LDS_CACHE_OFFSET + k) * stride]; }
     PS_D lds_float &stash(int k) const { return base[(LDS_STASH_OFFSET + k) * stride]; }
     // Stack: the stash in global memory ([GSTASH_PAIR_OFFSET][stride] floats, this env's column)
+    // (wave-uniform base and stride, the lane's byte offset: global_* v_off, s[base])
     float *gst = nullptr;
     int64_t gst_stride = 0;
+    uint32_t goff = 0;
     // Stack: this env's pair rows, env-major after the stash rows
     // ([stride][NP * PAIR_FLOATS]): one lane pointer plus immediate offsets
     __attribute__((address_space(1))) float *gpair = nullptr;
-    PS_D float &gstash(int k) const { return gst[k * gst_stride]; }
+    PS_D float &gstash(int k) const {
+        float *row = gst + k * gst_stride;
+        asm("" : "+s"(row));  // no reassociation into a per-lane pointer (StateView::at)
+        return *(float *)((char *)row + goff);
+    }
     // Stack only: ground row c of cube c / NG, field k (r.xyz, rhs[3])
     PS_D lds_float &gnd(int c, int k) const { return base[(LDS_GND_OFFSET + c * LDS_GND_FLOATS + k) * stride]; }
     // Stack only (global stash): pair row c, field k (dir[3].xyz, r0.xyz, r1.xyz, rhs[3], dinv[3]);
@@ -633,7 +639,7 @@ struct MJStore {
     PS_D MJStore opaque() const {
         MJStore r = *this;
         asm volatile("" : "+v"(r.base));
-        asm volatile("" : "+v"(r.gst));
+        asm volatile("" : "+v"(r.goff));
         asm volatile("" : "+v"(r.gpair));
         return r;
     }
@@ -814,8 +820,10 @@ struct WarmCache {
     MJStore lds;
     PS_D static int slot(int row) { return row < PS_F_WG1 ? row - PS_F_WG0 : 5 + (row - PS_F_WR); }
     PS_D float &at(int row) const {
-        int64_t e = ((int64_t)blockIdx.x * 64 + (int)__lane_id()) / G;
-        return base[(int64_t)(row - PS_F_WG0) * stride + e];
+        // a 32-bit byte offset from a wave-uniform row base (ps_create caps
+        // the batch at PS_MAX_ENVS), as StateView
+        const uint32_t e = (uint32_t)(((uint64_t)blockIdx.x * 64 + __lane_id()) / G) * 4u;
+        return *(float *)((char *)(base + (int64_t)(row - PS_F_WG0) * stride) + e);
     }
     PS_D float load(int row) const {
         if constexpr (IN_LDS) return lds.cache(slot(row));

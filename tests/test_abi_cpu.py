@@ -73,6 +73,10 @@ def test_create_and_dims_without_gpu(L):
     assert lib.ps_obs_dim(ctx) == 6 and lib.ps_action_dim(ctx) == 7
     lib.ps_destroy(ctx)
     assert lib.ps_create(C.byref(cfg), 0, 0, C.byref(ctx)) < 0
+    # the kernels address state rows by a 32-bit byte offset: PS_MAX_ENVS = 2^28
+    assert lib.ps_create(C.byref(cfg), (1 << 28) + 1, 0, C.byref(ctx)) < 0
+    assert lib.ps_create(C.byref(cfg), 1 << 28, 0, C.byref(ctx)) == 0
+    lib.ps_destroy(ctx)
     # goal sizes and TimeLimits of every task (__init__.py:18-46)
     dims = {0: (6, 3, 50), 1: (18, 3, 50), 2: (19, 3, 50), 3: (18, 3, 50), 4: (31, 6, 100), 5: (20, 4, 50)}
     for task, (obs, goal, steps) in dims.items():
