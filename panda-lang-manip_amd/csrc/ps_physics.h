@@ -1564,7 +1564,12 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     unsigned gate_ground[NB];
 #pragma unroll
     for (int b = 0; b < NB; b++) gate_ground[b] = wave_bits([&](int c) { return c < ng[b]; }, NG);
+#ifdef PS_DIAG_NO_PAIR_ROWS
+    // diagnostic only (wrong physics): the solver skips the box-box rows
+    const unsigned gate_pair = 0u;
+#else
     const unsigned gate_pair = wave_bits([&](int c) { return c < np; }, NP);
+#endif
     const unsigned gate_robot = wave_bits([&](int c) { return c < nr; }, NR);
 
 #ifdef PS_PROFILE_PHASES
@@ -1706,7 +1711,29 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     }
 
     auto contacts = [&]() {
-        // normals: ground contacts, pair contacts, then gripper contacts
+        // normals: ground contacts, pair contacts, then gripper contacts.
+        // Stack: the pair rows' read-only data come from the global stash
+        // (PAIR_FLOATS).  Every slot's loads are issued here, before the
+        // ground rows, so their L2 latency runs under those rows and the wave
+        // waits once per sweep, not once per contact (unused slots hold
+        // all-zero rows).
+        float pf[NP][11];
+        if constexpr (NOBJ == 2) {
+            if (gate_pair) {
+#pragma unroll
+                for (int c = 0; c < NP; c++) {
+#pragma unroll
+                    for (int k = 0; k < 3; k++) {
+                        pf[c][k] = L.pair(c, k);
+                        pf[c][3 + k] = L.pair(c, 9 + k);
+                        pf[c][6 + k] = L.pair(c, 12 + k);
+                    }
+                    pf[c][9] = L.pair(c, 15);
+                    pf[c][10] = L.pair(c, 18);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
 #pragma unroll
         for (int b = 0; b < NOBJ; b++) {
             const float inv_m = od[b].inv_m;
@@ -1740,22 +1767,24 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 }
         }
         if constexpr (NOBJ == 2) {
+            if (gate_pair) {
 #pragma unroll
-            for (int c = 0; c < NP; c++)
-                if (gate_pair & (1u << c)) {
-                    PairContact &p = pc[c];
-                    // Stack: the row's read-only data come from the global stash (PAIR_FLOATS)
-                    auto pv = [&](int k) { return mk(L.pair(c, k), L.pair(c, k + 1), L.pair(c, k + 2)); };
-                    const float sg = p.a0 ? 1.0f : -1.0f;  // A = object 0: +1
-                    const V3 d0 = pv(0), rn0 = cross(pv(9), d0), rn1 = cross(pv(12), d0);
-                    float jv = sg * pair_rel(rn0, rn1, d0);
-                    float dl = (float)L.pair(c, 15) - (float)L.pair(c, 18) * jv;
-                    float nl = fminf(fmaxf(p.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
-                    dl = nl - p.lam[0];
-                    p.lam[0] = nl;
-                    pair_apply(rn0, rn1, d0, sg * dl);
-                    res = fmaxf(res, row_viol(dl, L.pair(c, 18)));
-                }
+                for (int c = 0; c < NP; c++)
+                    if (gate_pair & (1u << c)) {
+                        PairContact &p = pc[c];
+                        const float sg = p.a0 ? 1.0f : -1.0f;  // A = object 0: +1
+                        const V3 d0 = mk(pf[c][0], pf[c][1], pf[c][2]);
+                        const V3 rn0 = cross(mk(pf[c][3], pf[c][4], pf[c][5]), d0);
+                        const V3 rn1 = cross(mk(pf[c][6], pf[c][7], pf[c][8]), d0);
+                        float jv = sg * pair_rel(rn0, rn1, d0);
+                        float dl = pf[c][9] - pf[c][10] * jv;
+                        float nl = fminf(fmaxf(p.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
+                        dl = nl - p.lam[0];
+                        p.lam[0] = nl;
+                        pair_apply(rn0, rn1, d0, sg * dl);
+                        res = fmaxf(res, row_viol(dl, pf[c][10]));
+                    }
+            }
         }
 #pragma unroll
         for (int c = 0; c < NR; c++)
@@ -1796,7 +1825,22 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 }
                 res = fmaxf(res, row_viol(dl, r.dinv[0]));
             }
-        // friction cones
+        // friction cones (Stack: the pair rows' loads first, as above)
+        float pq[NP][16];
+        if constexpr (NOBJ == 2) {
+            if (gate_pair) {
+#pragma unroll
+                for (int c = 0; c < NP; c++) {
+#pragma unroll
+                    for (int k = 0; k < 12; k++) pq[c][k] = L.pair(c, 3 + k);  // d1, d2, r0, r1
+                    pq[c][12] = L.pair(c, 16);
+                    pq[c][13] = L.pair(c, 17);
+                    pq[c][14] = L.pair(c, 19);
+                    pq[c][15] = L.pair(c, 20);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
 #pragma unroll
         for (int b = 0; b < NOBJ; b++) {
             const float inv_m = od[b].inv_m;
@@ -1845,32 +1889,33 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         }
         if constexpr (NOBJ == 2) {
             const float pmu = sc.fric * sc.fric;
+            if (gate_pair) {
 #pragma unroll
-            for (int c = 0; c < NP; c++)
-                if (gate_pair & (1u << c)) {
-                    PairContact &p = pc[c];
-                    // Stack: the row's read-only data come from the global stash (PAIR_FLOATS)
-                    auto pv = [&](int k) { return mk(L.pair(c, k), L.pair(c, k + 1), L.pair(c, k + 2)); };
-                    const float sg = p.a0 ? 1.0f : -1.0f;
-                    const V3 d1 = pv(3), d2 = pv(6), r0 = pv(9), r1 = pv(12);
-                    const V3 rn01 = cross(r0, d1), rn02 = cross(r0, d2), rn11 = cross(r1, d1), rn12 = cross(r1, d2);
-                    float ja = sg * pair_rel(rn01, rn11, d1);
-                    float jb = sg * pair_rel(rn02, rn12, d2);
-                    float dla = (float)L.pair(c, 16) - (float)L.pair(c, 19) * ja, dlb = (float)L.pair(c, 17) - (float)L.pair(c, 20) * jb;
-                    float sa = p.lam[1] + dla, sb = p.lam[2] + dlb;
-                    float lim = pmu * fmaxf(p.lam[0], 0.0f);
-                    float m2 = sa * sa + sb * sb;
-                    float s = cone_scale(m2, lim);
-                    sa *= s;
-                    sb *= s;
-                    dla = sa - p.lam[1];
-                    dlb = sb - p.lam[2];
-                    p.lam[1] = sa;
-                    p.lam[2] = sb;
-                    pair_apply(rn01, rn11, d1, sg * dla);
-                    pair_apply(rn02, rn12, d2, sg * dlb);
-                    res = fmaxf(res, fmaxf(row_viol(dla, L.pair(c, 19)), row_viol(dlb, L.pair(c, 20))));
-                }
+                for (int c = 0; c < NP; c++)
+                    if (gate_pair & (1u << c)) {
+                        PairContact &p = pc[c];
+                        auto pv = [&](int k) { return mk(pq[c][k], pq[c][k + 1], pq[c][k + 2]); };
+                        const float sg = p.a0 ? 1.0f : -1.0f;
+                        const V3 d1 = pv(0), d2 = pv(3), r0 = pv(6), r1 = pv(9);
+                        const V3 rn01 = cross(r0, d1), rn02 = cross(r0, d2), rn11 = cross(r1, d1), rn12 = cross(r1, d2);
+                        float ja = sg * pair_rel(rn01, rn11, d1);
+                        float jb = sg * pair_rel(rn02, rn12, d2);
+                        float dla = pq[c][12] - pq[c][14] * ja, dlb = pq[c][13] - pq[c][15] * jb;
+                        float sa = p.lam[1] + dla, sb = p.lam[2] + dlb;
+                        float lim = pmu * fmaxf(p.lam[0], 0.0f);
+                        float m2 = sa * sa + sb * sb;
+                        float s = cone_scale(m2, lim);
+                        sa *= s;
+                        sb *= s;
+                        dla = sa - p.lam[1];
+                        dlb = sb - p.lam[2];
+                        p.lam[1] = sa;
+                        p.lam[2] = sb;
+                        pair_apply(rn01, rn11, d1, sg * dla);
+                        pair_apply(rn02, rn12, d2, sg * dlb);
+                        res = fmaxf(res, fmaxf(row_viol(dla, pq[c][14]), row_viol(dlb, pq[c][15])));
+                    }
+            }
         }
 #pragma unroll
         for (int c = 0; c < NR; c++)
