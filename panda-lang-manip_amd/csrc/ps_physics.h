@@ -1747,7 +1747,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         const int at = b * NG + c;
                         gr = mk(L.gnd(at, 0), L.gnd(at, 1), L.gnd(at, 2));
                         grhs = L.gnd(at, 3);
-                        gdinv = cube_ground_dinv(gr, 0, od[b].iI, inv_m);
+                        // a slot this env does not have (the gate is the wave's) gets
+                        // 1/den = 0, so its rows stay exact no-ops: with the zeroed
+                        // offset alone, 1/den would be the cube's mass and the row
+                        // would push back on any downward velocity change
+                        gdinv = c < ng[b] ? cube_ground_dinv(gr, 0, od[b].iI, inv_m) : 0.0f;
                     }
                     V3 rn = mk(gr.y, -gr.x, 0.0f);  // r x (0,0,1); zero terms dropped below
                     float dl = grhs - gdinv * (rn.x * dw[b].x + rn.y * dw[b].y + dvl[b].z);
@@ -1855,8 +1859,9 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         gr = mk(L.gnd(at, 0), L.gnd(at, 1), L.gnd(at, 2));
                         grhs1 = L.gnd(at, 4);
                         grhs2 = L.gnd(at, 5);
-                        gdinv1 = cube_ground_dinv(gr, 1, od[b].iI, inv_m);
-                        gdinv2 = cube_ground_dinv(gr, 2, od[b].iI, inv_m);
+                        const bool on = c < ng[b];  // as in the normal sweep
+                        gdinv1 = on ? cube_ground_dinv(gr, 1, od[b].iI, inv_m) : 0.0f;
+                        gdinv2 = on ? cube_ground_dinv(gr, 2, od[b].iI, inv_m) : 0.0f;
                     }
                     V3 r1 = mk(gr.z, 0.0f, -gr.x);  // r x (0,-1,0)
                     V3 r2 = mk(0.0f, gr.z, -gr.y);  // r x (1,0,0)

@@ -527,6 +527,36 @@ def test_box_on_box_parity(ps):
     assert (e_obj < 1e-3).mean() >= 0.95 and e_obj.max() < 1e-2
 
 
+def test_airborne_cube_has_no_ground_rows(ps):
+    """Stack's ground-row gates are per wave: lanes whose cube has no ground
+    contact still run the rows some other lane of the wave has.  Those rows
+    must be exact no-ops.  Half the wave rests both cubes on the table (the
+    gates open); the other half holds the pair 0.3 m up with cube 2 sunk 3 mm
+    into cube 1, so the pair rows push cube 1 down in the solve.  A ground row
+    left live there would push back (its 1/den is the cube's mass at a zero
+    offset); against the oracle, the airborne cubes must match."""
+    B = 64
+    env = make_env(ps, "stack", "ee", B)
+    env.autoreset = False
+    env.reset(seed=5)
+    p1 = env.sim.get_base_position("object1").double()
+    air = torch.arange(B, device=p1.device) >= B // 2
+    p1[air, 2] = 0.3
+    p2 = p1.clone()
+    p2[:, 2] = p1[:, 2] + 0.04 - torch.where(air, 0.003, 0.0)
+    q = torch.zeros(B, 4, dtype=torch.float64, device=p1.device)
+    q[:, 3] = 1.0
+    env.sim.set_base_pose("object1", p1, q)
+    env.sim.set_base_pose("object2", p2, q)
+    cfg = oracle_config_for(env.sim.cfg)
+    up = np.zeros((B, env.action_dim), np.float32)
+    up[:, 2] = 1.0
+    e_obj, _ = _teacher_forced_objects(env, cfg, lambda s: up, 2, stride=1)
+    e_air = e_obj.reshape(-1, B)[:, B // 2:]  # (step, env) order
+    print("airborne pair", f"max obj err {np.max(e_air):.1e} (all lanes {np.max(e_obj):.1e})")
+    assert np.max(e_air) < 1e-3
+
+
 @pytest.mark.parametrize("task", OBJECT_TASKS)
 def test_gripper_object_contact_parity(ps, task):
     """Scripted pushes into the object (P-control of the end effector towards
