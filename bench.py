@@ -7,8 +7,10 @@ envs per GPU (weak scaling; 524 288 at 8 GPUs), env i of rank r seeded with
 0xC0FFEE + rank, auto-reset on terminated|truncated.  One "step" = one fused
 RobotTaskEnv.step() of every env (20 physics substeps + IK + obs + reward).
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU, RCCL).  Rank 0 prints one JSON line.
+Launch: python bench.py [--gpus N --steps K --warmup W].  For N > 1 the
+script starts `torch.distributed.run --nproc-per-node N` as a child process
+(one rank per GPU, RCCL) unless it already runs under torch.distributed.run
+(WORLD_SIZE set, which must equal N).  Rank 0 prints one JSON line.
 """
 from __future__ import annotations
 
@@ -209,6 +211,20 @@ def load_pmc(workload: str, key: str = "bytes_per_launch"):
         return None
 
 
+def launch_command(n: int, argv) -> list:
+    """The child command of `bench.py --gpus N` (N > 1): torch.distributed.run
+    with one process per GPU on this node, rendezvous on 127.0.0.1, each rank
+    running this script with the same arguments."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    argv = [a for a in argv if a != "--print-launch"]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -219,12 +235,33 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--lanes", type=int, default=0, help="lanes per env of the step kernel: 1, 8, 16, 0 = auto")
+    ap.add_argument("--print-launch", action="store_true",
+                    help="print the child command that --gpus N > 1 would start, and exit")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (args.gpus > 1 or args.print_launch):
+        # N ranks requested from a plain `python bench.py --gpus N`: start them as
+        # a child torch.distributed.run (one process per GPU) before anything
+        # here touches the GPU, wait for it and exit with its status
+        cmd = launch_command(args.gpus, sys.argv[1:])
+        if args.print_launch:
+            print(json.dumps({"launch": cmd}))
+            return
+        import subprocess
+
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        raise SystemExit(subprocess.run(cmd, env=env).returncode)
+    world = int(env_world or "1")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch one rank per GPU "
+                         f"(plain `python bench.py --gpus {args.gpus}` starts them)")
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; the modulo only matters when rehearsing N ranks on
@@ -240,6 +277,8 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
 
     import pandasim
     from pandasim.dist import EpisodeStats, gather_to_rank0, max_over_ranks, shard_seeds
@@ -293,7 +332,7 @@ def main():
         "metric": "env steps/sec (batched) PandaPush-v3 at 1/2/4/8 MI355X vs PyBullet CPU",
         "value": round(value, 1),
         "unit": "env-steps/s",
-        "n_gpus": world,
+        "n_gpus": dist.get_world_size() if world > 1 else 1,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),

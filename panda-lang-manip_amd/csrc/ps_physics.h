@@ -541,7 +541,7 @@ constexpr int NR = PM_MAX_ROBOT_CONTACTS;
 constexpr int NP = PM_MAX_PAIR_CONTACTS;
 // LDS floats per lane: M^-1 J^T of the 3 rows of every gripper contact
 // (108 floats x 256 lanes per CU = 108 KiB of the 160 KiB LDS at one wave per
-// SIMD); the diagnostic PS_MI_LDS build appends the packed M^-1.
+// SIMD).
 // Then 40 floats of per-substep values the PGS loop never reads (q, v1, the
 // split-impulse position correction, object 1's pre-solve velocities and
 // pose): they wait in LDS across the solve instead of holding registers.
@@ -553,13 +553,8 @@ constexpr int LDS_STASH_FLOATS = 40;
 // back once (run_substeps), not read and written through L2 every substep.
 constexpr int LDS_CACHE_OFFSET = LDS_STASH_OFFSET + LDS_STASH_FLOATS;
 constexpr int LDS_CACHE_FLOATS = 10;
-constexpr int LDS_MI_OFFSET = LDS_CACHE_OFFSET + LDS_CACHE_FLOATS;
-#ifdef PS_MI_LDS
-constexpr int LDS_FLOATS = LDS_MI_OFFSET + 45;
-#else
-constexpr int LDS_FLOATS = LDS_MI_OFFSET;
+constexpr int LDS_FLOATS = LDS_CACHE_OFFSET + LDS_CACHE_FLOATS;
 static_assert(LDS_FLOATS * 4 * 64 * 4 <= 160 * 1024, "four workgroups per CU");
-#endif
 // Stack (two cubes) keeps in LDS the gripper rows' J (the slots the other
 // scenes use for M^-1 J^T; the loop forms M^-1 J^T from the M^-1 registers)
 // and both cubes' ground rows (r, rhs: 6 per contact; 1/den is rebuilt from r,
@@ -612,7 +607,6 @@ struct MJStore {
     lds_float *base;
     int stride;
     PS_D lds_float &at(int slot, int row, int k) const { return base[((slot * 3 + row) * 9 + k) * stride]; }
-    PS_D lds_float &mi(int k) const { return base[(LDS_MI_OFFSET + k) * stride]; }
     PS_D lds_float &cache(int k) const { return base[(LDS_CACHE_OFFSET + k) * stride]; }
     PS_D lds_float &stash(int k) const { return base[(LDS_STASH_OFFSET + k) * stride]; }
     // Stack: the stash in global memory ([GSTASH_PAIR_OFFSET][stride] floats, this env's column)
@@ -1133,16 +1127,6 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     // M^-1 for the joint rows stays in registers: re-reading it from LDS in
     // every PGS iteration exposed the LDS latency once per motor row (Push
     // 4.56 -> 3.99 ms, Reach 2.97 -> 1.98 ms per step of 65 536 envs).
-    // PS_MI_LDS keeps the LDS variant for comparison.
-#ifdef PS_MI_LDS
-    constexpr bool MI_REGS = false;
-#else
-    constexpr bool MI_REGS = true;
-#endif
-    if constexpr (!MI_REGS) {
-#pragma unroll
-        for (int k = 0; k < 45; k++) lds.mi(k) = Mi[k];
-    }
     float v1[9];
 #pragma unroll
     for (int a = 0; a < 9; a++) {
@@ -1397,7 +1381,6 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 if (s == nr) slot[s] = c;
             nr++;
         };
-#ifndef PS_DBG_NO_RC
 #pragma unroll
         for (int b = 0; b < NOBJ; b++) {
             static_for<0, PM_NUM_SPHERES>([&](auto SS) {
@@ -1425,7 +1408,6 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 }
             }
         });
-#endif
         // 2) rows of each used slot: J (registers), M^-1 J^T (LDS), rhs, bounds;
         //    the normal starts from the cached impulse of the same feature
         float prl[NR];
@@ -1564,12 +1546,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     unsigned gate_ground[NB];
 #pragma unroll
     for (int b = 0; b < NB; b++) gate_ground[b] = wave_bits([&](int c) { return c < ng[b]; }, NG);
-#ifdef PS_DIAG_NO_PAIR_ROWS
-    // diagnostic only (wrong physics): the solver skips the box-box rows
-    const unsigned gate_pair = 0u;
-#else
     const unsigned gate_pair = wave_bits([&](int c) { return c < np; }, NP);
-#endif
     const unsigned gate_robot = wave_bits([&](int c) { return c < nr; }, NR);
 
 #ifdef PS_PROFILE_PHASES
@@ -1587,14 +1564,9 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         dl = nl - lam;
         lam = nl;
         float f = sgn * dl;
-        if constexpr (MI_REGS) {
 #pragma unroll
-            for (int a = 0; a < 9; a++) dv[a] += Mi[sidx(a, d)] * f;
-        } else {
-#pragma unroll
-            for (int a = 0; a < 9; a++) dv[a] += L.mi(sidx(a, d)) * f;
-        }
-        res = fmaxf(res, joint_viol(dl, MI_REGS ? Mi[sidx(d, d)] : (float)L.mi(sidx(d, d))));
+        for (int a = 0; a < 9; a++) dv[a] += Mi[sidx(a, d)] * f;
+        res = fmaxf(res, joint_viol(dl, Mi[sidx(d, d)]));
     };
     auto limit_row = [&](int d) {
         if (gate_lim & (1u << d)) {

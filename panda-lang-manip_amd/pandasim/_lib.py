@@ -73,13 +73,41 @@ def exported_symbols():
     ]
 
 
+def check_fresh(path: str) -> None:
+    """Refuse a library built from other sources than the ones next to it
+    (build.py's content stamp).  The product library and the named variants
+    (libpandasim_<variant>.so) must carry a stamp equal to the sha256 of the
+    current csrc/ and include/ files plus their flags; a library at any other
+    path (an experiment under PANDASIM_LIB) is checked only if it has a stamp
+    and its variant is known."""
+    from . import build as B
+
+    name = os.path.basename(path)
+    variant = None
+    if os.path.abspath(path) == os.path.abspath(B.OUT):
+        variant = ""
+    elif name.startswith("libpandasim_") and name.endswith(".so") and name[12:-3] in B.VARIANTS:
+        variant = name[12:-3]
+    if variant is None or not os.path.isdir(B.CSRC):
+        return
+    have = B.read_stamp(path)
+    if have is None:
+        if os.path.abspath(path) == os.path.abspath(B.OUT):
+            raise PandasimError(f"{path} has no build stamp: rebuild it with `python -m pandasim.build`")
+        return
+    if have != B.fingerprint(variant):
+        raise PandasimError(f"{path} is stale: its stamp does not match the sources in {B.CSRC} and "
+                            f"{B.INCLUDE}; rebuild it with `python -m pandasim.build`")
+
+
 def lib():
-    """Load libpandasim.so (raises if it has not been built)."""
+    """Load libpandasim.so (raises if it has not been built or is stale)."""
     global _lib
     if _lib is not None:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise PandasimError(f"{LIB_PATH} not found: build it with `python -m pandasim.build` (hipcc, gfx950)")
+    check_fresh(LIB_PATH)
     L = C.CDLL(LIB_PATH)
     V, I, I64, P = C.c_void_p, C.c_int, C.c_int64, C.POINTER
     L.ps_abi_version.restype = I

@@ -1,6 +1,20 @@
-"""Build libpandasim.so in-tree with hipcc for gfx950 (no JIT, no torch extension)."""
+"""Build libpandasim.so in-tree with hipcc for gfx950 (no JIT, no torch extension).
+
+The library is linked from parallel hipcc jobs (csrc/ps_env.h): the C ABI and
+small kernels (pandasim.hip), the fused step kernels of each (task, control)
+pair (step_kernels.hip, 12 objects) and the plugin-path substep kernel of each
+scene (sim_kernels.hip, 4 objects).
+
+Freshness is decided by content, not mtimes: every build writes
+``<lib>.sha256``, the sha256 of every source and header the library is built
+from plus the compile flags.  ``needs_build`` recomputes it, and
+``pandasim._lib.lib()`` refuses a library whose stamp does not match the
+sources next to it (a stale prebuilt .so shipped with the tree).
+"""
 from __future__ import annotations
 
+import concurrent.futures as cf
+import hashlib
 import os
 import subprocess
 import sys
@@ -8,47 +22,119 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
+INCLUDE = os.path.join(ROOT, "include")
 OUT = os.path.join(HERE, "libpandasim.so")
-SOURCES = ["pandasim.hip"]
+OBJ_DIR = os.path.join(HERE, "build")
 
+# -fno-slp-vectorize: SLP packing into v_pk_fma_f32 pairs made the register
+# allocator spill 590 VGPRs of the step kernel to scratch
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC", "-I", INCLUDE]
 
-def deps() -> list:
-    """Every source the library is built from: all of csrc/ (the kernels
-    include each header there) and the two public headers."""
-    return sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".h")))
-
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("pandasim.h", "panda_model.h")]
-
+# (object name, source, defines)
+UNITS = ([("pandasim", "pandasim.hip", [])]
+         + [(f"step_t{t}_c{c}", "step_kernels.hip", [f"-DPS_STEP_TASK={t}", f"-DPS_STEP_CONTROL={c}"])
+            for t in range(6) for c in range(2)]
+         + [(f"sim_{n}_{s}", "sim_kernels.hip", [f"-DPS_SIM_NOBJ={n}", f"-DPS_SIM_SHAPE={s}"])
+            for n, s in ((0, 0), (1, 0), (1, 1), (2, 0))])
 
 # diagnostic variants (never loaded by the product unless PANDASIM_LIB names them)
 VARIANTS = {"": [], "prof": ["-DPS_PROFILE_PHASES"]}
+
+
+def headers() -> list:
+    """Every header the objects include: csrc/*.h and include/*.h."""
+    hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
+    hs += [os.path.join(INCLUDE, f) for f in os.listdir(INCLUDE) if f.endswith(".h")]
+    return sorted(hs)
+
+
+def deps() -> list:
+    """Every source the library is built from."""
+    return sorted(headers() + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".hip")])
+
+
+def _digest(paths, flags) -> str:
+    h = hashlib.sha256()
+    for p in paths:
+        h.update(os.path.relpath(p, ROOT).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    h.update(" ".join(flags).encode())
+    return h.hexdigest()
 
 
 def out_path(variant: str = "") -> str:
     return OUT if not variant else os.path.join(HERE, f"libpandasim_{variant}.so")
 
 
-def needs_build(variant: str = "") -> bool:
-    out = out_path(variant)
-    if not os.path.exists(out):
-        return True
-    t = os.path.getmtime(out)
-    return any(os.path.getmtime(p) > t for p in deps() + HEADERS)
+def stamp_path(lib_path: str) -> str:
+    return lib_path + ".sha256"
 
 
-def build(force: bool = False, verbose: bool = True, variant: str = "", extra=()) -> str:
-    out = out_path(variant)
-    if not force and not extra and not needs_build(variant):
+def fingerprint(variant: str = "", extra=()) -> str:
+    """sha256 of every source and header plus the flags of `variant`."""
+    return _digest(deps(), FLAGS + VARIANTS[variant] + list(extra))
+
+
+def read_stamp(lib_path: str):
+    try:
+        with open(stamp_path(lib_path)) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def needs_build(variant: str = "", extra=(), out: str | None = None) -> bool:
+    out = out or out_path(variant)
+    return not os.path.exists(out) or read_stamp(out) != fingerprint(variant, extra)
+
+
+def _jobs() -> int:
+    for k in ("MAX_JOBS", "PANDASIM_BUILD_JOBS"):
+        v = os.environ.get(k)
+        if v and v.isdigit() and int(v) > 0:
+            return min(int(v), 16)
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def build(force: bool = False, verbose: bool = True, variant: str = "", extra=(), out: str | None = None) -> str:
+    out = out or out_path(variant)
+    want = fingerprint(variant, extra)
+    if not force and os.path.exists(out) and read_stamp(out) == want:
         return out
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    # -fno-slp-vectorize: SLP packing into v_pk_fma_f32 pairs made the register
-    # allocator spill 590 VGPRs of the step kernel to scratch (DESIGN.md §4)
-    cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize", "-fPIC", "-shared", "-I", os.path.join(ROOT, "include"),
-           *VARIANTS[variant], *extra, "-o", out + ".tmp"] + [os.path.join(CSRC, s) for s in SOURCES]
+    tag = os.path.splitext(os.path.basename(out))[0]
+    odir = os.path.join(OBJ_DIR, tag)
+    os.makedirs(odir, exist_ok=True)
+    hdrs = headers()
+    flags = FLAGS + VARIANTS[variant] + list(extra)
+
+    def compile_unit(unit):
+        name, src, defs = unit
+        obj = os.path.join(odir, name + ".o")
+        # an object is reused when its own source, every header and its flags are unchanged
+        key = _digest(hdrs + [os.path.join(CSRC, src)], flags + defs)
+        if not force and os.path.exists(obj) and read_stamp(obj) == key:
+            return obj
+        cmd = [hipcc, *flags, *defs, "-c", "-o", obj + ".tmp", os.path.join(CSRC, src)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(obj + ".tmp", obj)
+        with open(stamp_path(obj), "w") as f:
+            f.write(key + "\n")
+        return obj
+
+    with cf.ThreadPoolExecutor(_jobs()) as ex:
+        objs = list(ex.map(compile_unit, UNITS))
+    cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(out + ".tmp", out)
+    with open(stamp_path(out), "w") as f:
+        f.write(want + "\n")
     return out
 
 

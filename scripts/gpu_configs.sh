@@ -1,13 +1,23 @@
 # GPU pass: the bench line at every BASELINE config that fits one GPU
-# (SURVEY.md §8(d)), plus the default bench line with its CPU baseline.
+#  and every task at 65 536 envs -> gpurun_out/configs.jsonl;
+# LANES="1 8 16" adds a sweep of the step kernel's lanes per env over the
+# small-batch configs -> gpurun_out/lanes.jsonl;
+# VARIANTS=1 times the experimental builds of scripts/build_variants.py.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 || exit $?
-for cfg in "PandaReach-v3 4096" "PandaReachJoints-v3 4096" "PandaPush-v3 8192" "PandaPickAndPlace-v3 8192" \
-           "PandaPush-v3 65536" "PandaReachDense-v3 65536" "PandaReachJoints-v3 65536" "PandaPickAndPlace-v3 65536" \
-           "PandaSlide-v3 65536" "PandaStack-v3 65536" "PandaFlip-v3 65536"; do
-  set -- $cfg
-  timeout -k 10 300 python bench.py --no-cpu-baseline --env-id $1 --batch $2 >> gpurun_out/configs.jsonl 2>/dev/null || exit $?
+for cfg in ${CONFIGS:-"PandaReach-v3:4096 PandaReachJoints-v3:4096 PandaPush-v3:8192 PandaPickAndPlace-v3:8192 \
+           PandaPush-v3:65536 PandaReachDense-v3:65536 PandaReachJoints-v3:65536 PandaPickAndPlace-v3:65536 \
+           PandaSlide-v3:65536 PandaStack-v3:65536 PandaFlip-v3:65536"}; do
+  timeout -k 10 300 python bench.py --no-cpu-baseline --env-id ${cfg%%:*} --batch ${cfg##*:} >> gpurun_out/configs.jsonl 2>>gpurun_out/configs.err || exit $?
 done
-echo "done rc=$?"
+for lanes in $LANES; do
+  for cfg in PandaReach-v3:4096 PandaPush-v3:8192 PandaPickAndPlace-v3:8192 PandaPush-v3:16384; do
+    timeout -k 10 300 python bench.py --no-cpu-baseline --steps 40 --warmup 5 --env-id ${cfg%%:*} --batch ${cfg##*:} \
+      --lanes $lanes >> gpurun_out/lanes.jsonl 2>>gpurun_out/lanes.err || exit $?
+  done
+done
+if [ -n "$VARIANTS" ]; then
+  TASKS=reach,push,pick_and_place timeout -k 10 600 python scripts/time_variants.py scripts/bin/variants/*.so > gpurun_out/variants.log 2>&1 || exit $?
+fi
+echo "done rc=0"

@@ -151,3 +151,31 @@ def test_flop_model_counts():
     assert f["split"]["ik"] == 20 * R.IK_ITERATION
     assert f["pgs_iterations_per_substep"] == 30.0 and f["ik_iterations_per_step"] == 20.0
     assert f["flops_per_env_step"] == sum(f["split"].values())
+
+
+def test_build_freshness_is_decided_by_content_not_mtime():
+    """build.py's stamp: a header whose bytes change while its mtime does not
+    makes the library stale, and _lib refuses to load a stale library."""
+    from pandasim import _lib
+    from pandasim import build as B
+
+    assert not B.needs_build(), "build the library first (python -m pandasim.build)"
+    hdr = os.path.join(B.CSRC, "ps_common.h")
+    st = os.stat(hdr)
+    orig = open(hdr, "rb").read()
+    try:
+        with open(hdr, "wb") as f:
+            f.write(orig + b"// freshness probe\n")
+        os.utime(hdr, ns=(st.st_atime_ns, st.st_mtime_ns))
+        assert os.stat(hdr).st_mtime_ns == st.st_mtime_ns
+        assert B.needs_build()
+        with pytest.raises(_lib.PandasimError, match="stale"):
+            _lib.check_fresh(B.OUT)
+    finally:
+        with open(hdr, "wb") as f:
+            f.write(orig)
+        os.utime(hdr, ns=(st.st_atime_ns, st.st_mtime_ns))
+    assert not B.needs_build()
+    _lib.check_fresh(B.OUT)
+    # flags are part of the stamp too
+    assert B.fingerprint("") != B.fingerprint("prof") != B.fingerprint("", ["-DX"])

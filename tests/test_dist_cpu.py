@@ -106,3 +106,37 @@ def test_gloo_gather_reassembles_global_batch(world, B):
     assert torch.equal(torch.tensor(full), st.packed())
     assert seeds == [12345.0 + g for g in range(B)]
     assert t == float(world)
+
+
+# ---- bench.py's multi-rank launch (no GPU: these exit before importing torch)
+def _bench(args, env_extra=None):
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], capture_output=True, text=True,
+                          timeout=60, env=env, cwd=root)
+
+
+def test_bench_gpus_n_launches_n_ranks_as_a_child():
+    import json
+
+    out = _bench(["--gpus", "8", "--steps", "7", "--warmup", "2", "--print-launch"])
+    assert out.returncode == 0, out.stderr
+    cmd = json.loads(out.stdout.strip().splitlines()[-1])["launch"]
+    i = cmd.index("torch.distributed.run")
+    assert cmd[i - 1] == "-m"
+    assert cmd[cmd.index("--nproc-per-node") + 1] == "8"
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[cmd.index("--nnodes=1")]
+    script = cmd.index(next(a for a in cmd if a.endswith("bench.py")))
+    assert cmd[script + 1:] == ["--gpus", "8", "--steps", "7", "--warmup", "2"]
+
+
+def test_bench_refuses_world_size_other_than_gpus():
+    out = _bench(["--gpus", "1", "--steps", "1"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert out.returncode != 0 and "WORLD_SIZE=2" in (out.stderr + out.stdout)
+    out = _bench(["--gpus", "4", "--steps", "1"], {"WORLD_SIZE": "8", "RANK": "0", "LOCAL_RANK": "0"})
+    assert out.returncode != 0 and "--gpus 4" in (out.stderr + out.stdout)

@@ -30,9 +30,11 @@ def _json_line(stdout: str) -> dict:
 
 
 def test_bench_two_ranks_gloo_rehearsal():
+    # plain `python bench.py --gpus 2`, as the driver's N-GPU run may invoke it:
+    # bench.py itself starts the two ranks (torch.distributed.run child)
     env = dict(os.environ, PANDASIM_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "3", "--warmup", "1", "--batch", "256", "--no-cpu-baseline"]
     out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
     assert out.returncode == 0, out.stderr[-3000:]
@@ -41,6 +43,17 @@ def test_bench_two_ranks_gloo_rehearsal():
     assert line["config"]["global_batch"] == 512 and line["config"]["batch_per_gpu"] == 256
     assert line["episodes"]["gathered_envs"] == 512  # rank 0 holds both shards
     assert line["value"] > 0 and line["scaling"] == "weak"
+
+
+def test_bench_under_explicit_torchrun():
+    env = dict(os.environ, PANDASIM_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "128", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = _json_line(out.stdout)
+    assert line["n_gpus"] == 2 and line["episodes"]["gathered_envs"] == 256
 
 
 def test_bench_single_rank_roofline_blocks():
