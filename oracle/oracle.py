@@ -49,6 +49,10 @@ class Env(C.Structure):
         ("m_vel", C.c_double * 9), ("m_maximp", C.c_double * 9),
         ("obj", Body * 2), ("goal", C.c_double * 6), ("elapsed", C.c_int64), ("rng", C.c_uint64 * 5),
         ("cache", Cache),
+        # test bookkeeping (po_substep): discrete-state signature and its changes
+        ("event_sig", C.c_uint64), ("event_changes", C.c_int64),
+        ("finger_sig", C.c_uint64), ("finger_changes", C.c_int64),
+        ("contact_sig", C.c_uint64), ("limit_sig", C.c_uint64), ("event_kinds", C.c_int64),
     ]
 
 
@@ -114,6 +118,7 @@ def lib():
         L.po_link_inertia.argtypes = [I, P(D)]
         L.po_set_link_aabb.argtypes = [I, D, D, D]
         L.po_set_finger_noise.argtypes = [D, C.c_uint64]
+        L.po_set_state_noise.argtypes = [D, C.c_uint64]
         _lib = L
     return _lib
 
@@ -271,3 +276,9 @@ def set_finger_noise(amplitude: float, seed: int = 0):
 
 def set_link_aabb(link, lx, ly, lz):
     lib().po_set_link_aabb(link, lx, ly, lz)
+
+
+def set_state_noise(ulps: float, seed: int = 0):
+    """Test hook: fp32-resolution noise of u * ulp32(x), |u| <= ulps, on every
+    state component after each substep (panda_oracle.c po_set_state_noise)."""
+    lib().po_set_state_noise(float(ulps), int(seed))

@@ -1060,6 +1060,42 @@ static double finger_noise(void) {
     return finger_noise_amp * ((double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0);
 }
 
+/* Test hook (never part of the restated algorithm): fp32-resolution state
+ * noise.  After every substep each state component x moves by u * ulp32(x),
+ * u uniform in [-ulps, ulps], ulp32(x) = the spacing of float32 at |x|
+ * (2^(e - 24) for |x| = m 2^e, m in [0.5, 1)).  The free-run parity tests use
+ * it as the yardstick of how far apart two runs that differ by the state's
+ * fp32 rounding drift. */
+static double state_noise_ulps = 0.0;
+void po_set_state_noise(double ulps, uint64_t seed) {
+    state_noise_ulps = ulps;
+    finger_noise_state = seed ^ 0xA0761D6478BD642FULL;
+}
+static double unit_noise(void) {
+    uint64_t z = (finger_noise_state += 0x9E3779B97F4A7C15ULL);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    z ^= z >> 31;
+    return (double)(z >> 11) * (2.0 / 9007199254740992.0) - 1.0;
+}
+static void ulp_noise(double *x, int n) {
+    for (int k = 0; k < n; k++) {
+        if (x[k] == 0.0 || !isfinite(x[k])) continue;
+        int e;
+        frexp(x[k], &e);
+        x[k] += state_noise_ulps * unit_noise() * ldexp(1.0, e - 24);
+    }
+}
+
+/* Event signatures of a substep (test bookkeeping): the ordered contact
+ * features (cache group and id; object-object contacts by count) with the
+ * arm's joint-limit rows (joint and side), and separately the finger joints'
+ * limit rows, each hashed into 63 bits, bit 63 set. */
+static uint64_t sig_mix(uint64_t h, uint64_t v) {
+    h ^= v + 0x9E3779B97F4A7C15ULL + (h << 6) + (h >> 2);
+    return h;
+}
+
 /* One btMultiBodyDynamicsWorld::stepSimulation of 1/500 s
  * (pybullet.py:52-55 calls it 20 times per env step):
  *   1. forward dynamics velocity update qd1 = qd + h M^-1 (-bias)
@@ -1209,6 +1245,30 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
         r->lam = PM_WARMSTART_FACTOR * prev;
         for (int d = 0; d < ND; d++) dv[d] += r->MJ[d] * r->lam;
     }
+    {
+        uint64_t lsig = 0x243F6A8885A308D3ULL, fsig = 0x13198A2E03707344ULL, csig = 0xA4093822299F31D0ULL;
+        for (int j = 0; j < n_noncontact; j++)
+            if (rows[j].hi == PM_LIMIT_MAX_IMPULSE && rows[j].lo == 0.0)
+                for (int d = 0; d < 9; d++)
+                    if (rows[j].J[d] != 0.0) {
+                        uint64_t v = (uint64_t)(d * 2 + (rows[j].J[d] < 0.0)) + 1;
+                        if (d < 7) lsig = sig_mix(lsig, v);
+                        else fsig = sig_mix(fsig, v);
+                    }
+        for (int c = 0; c < nc; c++)
+            csig = sig_mix(csig, cts[c].group == CG_PAIR ? 2000 : (uint64_t)(cts[c].group * 64 + cts[c].id) + 3000);
+        uint64_t sig = sig_mix(lsig, csig) | (1ULL << 63);
+        fsig |= 1ULL << 63;
+        if (env->event_sig != 0 && env->event_sig != sig) {
+            env->event_changes++;
+            env->event_kinds |= (env->contact_sig != csig ? 1 : 0) | (env->limit_sig != lsig ? 2 : 0);
+        }
+        if (env->finger_sig != 0 && env->finger_sig != fsig) env->finger_changes++;
+        env->event_sig = sig;
+        env->finger_sig = fsig;
+        env->contact_sig = csig;
+        env->limit_sig = lsig;
+    }
     int it;
     for (it = 0; it < PM_SOLVER_ITERATIONS; it++) {
         double res = 0.0, x;
@@ -1259,6 +1319,10 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
         if (finger_noise_amp != 0.0)
             for (int d = 7; d < 9; d++) env->q[d] += finger_noise();
     }
+    if (state_noise_ulps != 0.0 && cfg->has_robot) {
+        ulp_noise(env->q, 9);
+        ulp_noise(env->qd, 9);
+    }
     for (int i = 0; i < cfg->n_objects; i++) {
         po_body *b = &env->obj[i];
         int o = OBJ_DOF(i);
@@ -1275,6 +1339,12 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
         quat_mul(dq, b->quat, nq);
         double nn = sqrt(nq[0] * nq[0] + nq[1] * nq[1] + nq[2] * nq[2] + nq[3] * nq[3]);
         for (int d = 0; d < 4; d++) b->quat[d] = nq[d] / nn;
+        if (state_noise_ulps != 0.0) {
+            ulp_noise(b->pos, 3);
+            ulp_noise(b->quat, 4);
+            ulp_noise(b->vel, 3);
+            ulp_noise(b->omg, 3);
+        }
     }
 }
 

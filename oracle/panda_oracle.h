@@ -83,6 +83,18 @@ typedef struct {
     int64_t elapsed;
     uint64_t rng[5]; /* PCG64 state hi, lo, inc hi, lo; splitmix64 state of Flip's goal stream */
     po_cache cache;
+    /* test bookkeeping, not physics: signature of the last substep's discrete
+     * state (contact features and the arm's joint-limit rows, 0 = none yet)
+     * and how many substeps changed it; the same for the two finger joints'
+     * limit rows (po_substep; the event-onset parity tests) */
+    uint64_t event_sig;
+    int64_t event_changes;
+    uint64_t finger_sig;
+    int64_t finger_changes;
+    /* which parts of event_sig have changed so far: bit 0 the contact
+     * features, bit 1 the arm's joint-limit rows */
+    uint64_t contact_sig, limit_sig;
+    int64_t event_kinds;
 } po_env;
 
 /* Work counters (bench.py's FLOP roofline): substeps, PGS
@@ -144,6 +156,10 @@ void po_link_inertia(int link, double inertia[3]);
 void po_set_link_aabb(int link, double lx, double ly, double lz);
 /* test hook: per-substep finger-position noise of +-amplitude (0 = off), not thread-safe */
 void po_set_finger_noise(double amplitude, uint64_t seed);
+/* test hook: after every substep each state component x (q, qd, object pose
+ * and velocities) moves by u * ulp32(x), u uniform in [-ulps, ulps] -- the
+ * fp32 resolution of the state (0 = off), not thread-safe */
+void po_set_state_noise(double ulps, uint64_t seed);
 
 #ifdef __cplusplus
 }

@@ -63,6 +63,11 @@ PS_DECLARE_SIM_LAUNCHER(2, 0)
 unsigned long long *ps_prof_buffer();
 #endif
 
+// minimum waves per SIMD the step kernels are register-allocated for
+#ifndef PS_STEP_MIN_WAVES
+#define PS_STEP_MIN_WAVES 1
+#endif
+
 namespace {
 
 
@@ -239,14 +244,24 @@ PS_D uint64_t &aux_rng(const StateView &s, int64_t i) { return s.R(4, i); }
 // the substeps; the plugin path's full rows (45 floats) are re-read from the
 // state at every substep instead of occupying registers through the solver
 // (the index goes through an empty asm so the loads stay in the loop).
-// STD_MOTORS: `tgt` holds the targets set_action computed in this lane (the
-// group kernels store them from one lane only, so no lane reads them back).
+// STD_MOTORS: `tgt` holds the targets set_action computed in this lane.
 template <int NOBJ, int SHAPE, bool STD_MOTORS, int G = 1>
 PS_D void run_substeps(const KParams &P, int64_t i, int n, float q[9], float qd[9], Body *bd,
                        const MJStore &lds, bool live, const float *tgt PS_PROF_PARAM) {
     static_assert(kBlock == 64, "WarmCache: one wave per workgroup");
     const WarmCache<G, NOBJ> wc{P.s.f + PS_F_WG0 * P.s.stride, P.s.stride, live, lds};
     wc.to_lds();
+    // G > 1: the targets come back from the state rows, which every lane of
+    // the group wrote with the same values (k_step); held in registers across
+    // the substeps the 8-lane Slide kernel drifted from the one-lane kernel by
+    // 2 cm (the lanes' dumped targets were identical: a codegen effect, not a
+    // per-lane difference), through memory it is bit-identical to it
+    float tgt_mem[9];
+    if constexpr (G > 1) {
+#pragma unroll
+        for (int d = 0; d < 9; d++) tgt_mem[d] = STD_MOTORS ? P.s.F(PS_F_MTARGET + d, i) : 0.0f;
+        tgt = tgt_mem;
+    }
     for (int st = 0; st < n; st++) {
         int64_t ii = i;
         asm volatile("" : "+v"(ii));
@@ -573,7 +588,7 @@ inline bool scene_matches_task(const ps_config &c) {
 // of the last wave past the batch end compute a copy of the last env and
 // write nothing.
 template <int TASK, int CONTROL, int G = 1>
-__global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions, float *obs, float *ag, float *dg,
+__global__ __launch_bounds__(kBlock, PS_STEP_MIN_WAVES) void k_step(KParams P, const float *actions, float *obs, float *ag, float *dg,
                                                  float *reward, uint8_t *terminated, uint8_t *truncated,
                                                  float *final_obs, float *final_ag) {
     using T = TaskTraits<TASK>;
@@ -597,10 +612,10 @@ __global__ __launch_bounds__(kBlock) void k_step(KParams P, const float *actions
     {
         Motors m;
         set_action<CONTROL>(P, actions + i * P.action_dim, q, m);
-        if (writer) {
-            store_motor_targets(s, i, m);
-            if (P.write_gains) store_motor_gains(s, i, m);
-        }
+        // every lane of a group stores the same targets (no lane reads a value
+        // only another lane wrote; run_substeps reads them back for G > 1)
+        if (G > 1 || writer) store_motor_targets(s, i, m);
+        if (writer && P.write_gains) store_motor_gains(s, i, m);
 #pragma unroll
         for (int d = 0; d < 9; d++) tgt[d] = m.target[d];
     }

@@ -33,3 +33,4 @@ int PS_STEP_LAUNCHER_NAME(PS_STEP_TASK, PS_STEP_CONTROL)(ps_ctx *c, void *state,
 #undef PS_LAUNCH
     return check_launch(c);
 }
+

@@ -60,7 +60,9 @@ def _digest(paths, flags) -> str:
         with open(p, "rb") as f:
             h.update(f.read())
         h.update(b"\0")
-    h.update(" ".join(flags).encode())
+    # flags with the tree's own location abstracted (the stamp must hold on the
+    # GPU box, where the same tree sits at another path)
+    h.update(" ".join(f.replace(ROOT, "<root>") for f in flags).encode())
     return h.hexdigest()
 
 

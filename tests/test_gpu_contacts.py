@@ -11,12 +11,14 @@ rollouts).
 * set_base_pose / reset place objects at rest (resetBasePositionAndOrientation
   zeroes the base velocity) and empty the cache.
 * Free runs: the fp32 GPU path and the fp64 oracle from the same initial
-  states and actions.  Contact and joint-limit events make these dynamics
-  chaotic, so the bound is stated against the oracle's own conditioning: the
-  fraction of env-steps within 1e-3 of the oracle must be at least the
-  fraction a second oracle run reaches when noise at the solver's resolution
-  is injected into its state every step (SOLVER_NOISE).
+  states and actions.  Before the first contact or joint-limit event of an
+  env the dynamics are smooth and the two must agree to 1e-5 m (event-onset
+  tests); after it they are chaotic, so the long-horizon bound is an absolute
+  floor plus the oracle's own conditioning at fp32 resolution (ULP_NOISE).
 """
+import copy
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -161,81 +163,208 @@ def test_reset_places_objects_at_rest(task):
             assert torch.all(env.sim.f[89:121, :B][:, done] == 0)
 
 
-# Noise of the fp64 comparison run, per step: the solver's own resolution.
-# PGS stops once every row's residual is below sqrt(1e-7) = 3.2e-4 (velocity
-# units), so two valid solutions of a substep differ by up to that much; the
-# fp32 and fp64 runs stop at different iterations and differ by ~1e-4 in
-# joint velocity after a step (test_sim_step_parity_same_motors).  Joint
-# positions get 1e-6, joint velocities 1e-4, object positions 1e-7 and object
-# velocities 1e-5 (absolute, Gaussian).
-SOLVER_NOISE = dict(q=1e-6, qd=1e-4, pos=1e-7, vel=1e-5)
+# Yardstick of the free runs: the fp64 oracle perturbed at the fp32
+# resolution of the state, one fp32 ulp per state component per substep
+# (oracle.set_state_noise).  A second oracle run with this noise shows how far
+# two runs that differ only by fp32 rounding of the state drift apart.
+ULP_NOISE = 1.0
+# Free-run floors (absolute, next to the relative yardstick): fraction of
+# env-steps whose ee/object positions are within 1e-3 m of the oracle, 64 envs
+# x 200 steps, seed 2024.  Measured in profiles/r03*_pytest_gpu.log.
+FREE_RUN_FLOOR = {("push", "ee"): 0.88, ("pick_and_place", "ee"): 0.72,
+                  ("reach", "joints"): 0.98, ("push", "joints"): 0.97}
+_RUNS = {}
 
 
-def _free_run(task, control, B, T, seed):
-    """GPU vs oracle free run: fraction of env-steps whose end-effector and
-    object positions agree within 1e-3 m, the worst error, and the same
-    fraction for a second oracle run perturbed by SOLVER_NOISE every step."""
+def _obs_index(task):
+    nobj = {"reach": 0, "stack": 2}.get(task, 1)
+    robot_dim = 6 if task in ("reach", "push", "slide") else 7  # + finger width (panda.py:109-119)
+    per = 13 if task == "flip" else 12
+    return nobj, [0, 1, 2] + [robot_dim + per * b + k for b in range(nobj) for k in range(3)]
+
+
+def _free_run(task, control, B=64, T=200, seed=2024, open_gripper=False):
+    """GPU vs oracle free run from the same initial states and actions.
+    Returns per env-step arrays [T, B]: the GPU's error against the oracle
+    (max over ee and object positions), the error of an oracle run perturbed
+    by ULP_NOISE, whether the reference oracle's discrete state (contact
+    features, joint-limit rows: po_env.event_sig) has changed at any substep
+    up to and including that step, and whether the GPU's contact-cache ids
+    equal the oracle's after that step."""
+    key = (task, control, B, T, seed, open_gripper)
+    if key in _RUNS:
+        return _RUNS[key]
     env = make_env(task, control, B)
     env.reset(seed=seed)
+    if open_gripper:
+        # fingers half open (0.02 m each, off both limits) and gripper action 0
+        # (width target = current width): no finger-limit branch is reachable
+        env.sim.f[7:9, :B] = 0.02
     cfg = oracle_config_for(env.sim.cfg)
     snap = snapshot(env.sim)
     ref = [oracle_env_from(cfg, snap, i) for i in range(B)]
     pert = [oracle_env_from(cfg, snap, i) for i in range(B)]
     rng = np.random.default_rng(seed)
-    nz = np.random.default_rng(seed + 1)
-    nobj = {"reach": 0, "stack": 2}.get(task, 1)
-    robot_dim = 6 if task in ("reach", "push", "slide") else 7  # + finger width (panda.py:109-119)
-    per = 13 if task == "flip" else 12
-    idx = [0, 1, 2] + [robot_dim + per * b + k for b in range(nobj) for k in range(3)]
-    within_gpu = within_noise = 0
-    worst = 0.0
-    N = SOLVER_NOISE
+    nobj, idx = _obs_index(task)
+    err_gpu = np.zeros((T, B))
+    err_ulp = np.zeros((T, B))
+    event = np.zeros((T, B), bool)
+    fevent = np.zeros((T, B), bool)
+    kinds = np.zeros((T, B), np.int8)
+    ids_equal = np.zeros((T, B), bool)
     for s in range(T):
         a = rng.uniform(-1, 1, size=(B, env.action_dim)).astype(np.float32)
+        if open_gripper:
+            a[:, -1] = 0.0
         obs, *_ = env.step(torch.from_numpy(a).cuda())
         og = obs["observation"].cpu().numpy()
+        f = env.sim.f[:, :B].double().cpu().numpy()
         for i in range(B):
             o, *_ = O.step(cfg, ref[i], a[i])
-            err = float(np.abs(og[i, idx] - o[idx]).max())
-            worst = max(worst, err)
-            within_gpu += err <= 1e-3
-            e = pert[i]
-            for d in range(9):
-                e.q[d] += N["q"] * nz.standard_normal()
-                e.qd[d] += N["qd"] * nz.standard_normal()
-            for b in range(nobj):
-                for k in range(3):
-                    e.obj[b].pos[k] += N["pos"] * nz.standard_normal()
-                    e.obj[b].vel[k] += N["vel"] * nz.standard_normal()
-                    e.obj[b].omg[k] += N["vel"] * nz.standard_normal()
-            op, *_ = O.step(cfg, e, a[i])
-            within_noise += float(np.abs(op[idx] - o[idx]).max()) <= 1e-3
-    n = B * T
-    return within_gpu / n, worst, within_noise / n
+            err_gpu[s, i] = np.abs(og[i, idx] - o[idx]).max()
+            event[s, i] = ref[i].event_changes > 0
+            fevent[s, i] = ref[i].finger_changes > 0
+            kinds[s, i] = ref[i].event_kinds
+            gc, oc = gpu_cache(f, i), oracle_cache(ref[i])
+            ids_equal[s, i] = all([k for k, _ in gc[g]] == [k for k, _ in oc[g]] for g in ("ground0", "ground1", "robot")) \
+                and len(gc["pair"]) == len(oc["pair"])
+            O.set_state_noise(ULP_NOISE, seed=(s * B + i) * 2 + 1)
+            op, *_ = O.step(cfg, pert[i], a[i])
+            O.set_state_noise(0.0)
+            err_ulp[s, i] = np.abs(op[idx] - o[idx]).max()
+    _RUNS[key] = (err_gpu, err_ulp, event, fevent, ids_equal)
+    os.makedirs("gpurun_out", exist_ok=True)
+    np.savez_compressed(f"gpurun_out/free_run_{task}_{control}{'_open' if open_gripper else ''}.npz", err_gpu=err_gpu,
+                        err_ulp=err_ulp, event=event, fevent=fevent, kinds=kinds, ids_equal=ids_equal)
+    return _RUNS[key]
 
 
-@pytest.mark.parametrize("task", ["push", "pick_and_place"])
-def test_free_running_200_steps_ee(task):
-    """The bench's control mode (ee, with the IK stopping rule) free-running
-    for 200 steps, 64 envs: end-effector and object positions of the fp32 GPU
-    path vs the fp64 oracle.  Contact and joint-limit events make the
-    trajectories chaotic (a finger at its limit flips branch at the 1e-22
-    level), so the bound is relative: the GPU run stays within
-    1e-3 of the oracle at least as often as an oracle run perturbed at the
-    solver's own resolution does."""
-    frac, worst, frac_noise = _free_run(task, "ee", 64, 200, seed=2024)
-    print(task, f"ee 200-step free run: {frac * 100:.2f} % of env-steps within 1e-3 (worst {worst:.1e} m); "
-                f"oracle vs oracle + solver-resolution noise: {frac_noise * 100:.2f} %")
-    assert frac >= frac_noise
+def _report(task, control, err_gpu, err_ulp, event):
+    pre = ~event
+    frac, frac_ulp = float((err_gpu <= 1e-3).mean()), float((err_ulp <= 1e-3).mean())
+    first = np.where(event.any(0), event.argmax(0), event.shape[0])
+    print(f"{task} {control}: GPU within 1e-3 of the oracle in {frac * 100:.2f} % of env-steps (worst "
+          f"{err_gpu.max():.1e} m); oracle + {ULP_NOISE:g} fp32 ulp/substep noise: {frac_ulp * 100:.2f} % "
+          f"(worst {err_ulp.max():.1e}); pre-event env-steps {int(pre.sum())} / {pre.size} (first event: median step "
+          f"{int(np.median(first))}), pre-event max error GPU {err_gpu[pre].max() if pre.any() else 0:.2e} m, "
+          f"oracle+ulp {err_ulp[pre].max() if pre.any() else 0:.2e} m")
+    return frac, frac_ulp
 
 
-@pytest.mark.parametrize("task", ["reach", "push"])
-def test_free_running_200_steps_joints(task):
-    """Joint control (no IK stopping rule), 200 steps, same criterion."""
-    frac, worst, frac_noise = _free_run(task, "joints", 64, 200, seed=2024)
-    print(task, f"joints 200-step free run: {frac * 100:.2f} % within 1e-3 (worst {worst:.1e} m); "
-                f"oracle vs oracle + solver-resolution noise: {frac_noise * 100:.2f} %")
-    assert frac >= frac_noise
+# Pre-event bound: until the first event the only difference between the
+# fp32 GPU run and the fp64 oracle is rounding, which the integrating ee
+# (targets are relative to the current position) accumulates as a random
+# walk over the event-free span.  The GPU must stay within an absolute bound
+# and within PRE_EVENT_ULP_RATIO x the deviation of an oracle run perturbed by
+# one fp32 ulp per state component per substep.  Measured
+# (profiles/r03*_pytest_gpu.log): 200-step runs Push 7.2e-6 m (oracle+ulp
+# 7.1e-6), PickAndPlace with the gripper held 5.5e-6 (8.0e-6) -- the 1e-5 m
+# of the north star; the bench config, whose event-free spans run up to a
+# 50-step episode, 2.0e-5 m (oracle+ulp 3.3e-5).
+PRE_EVENT_ULP_RATIO = 2.0
+
+
+def _check_pre_event(name, err_gpu, err_ulp, pre, abs_tol, ids_equal=None):
+    assert pre.sum() >= 0.05 * pre.size, f"{name}: too few pre-event env-steps for the check to mean anything"
+    g, u = float(err_gpu[pre].max()), float(err_ulp[pre].max())
+    print(f"{name}: pre-event env-steps {int(pre.sum())}/{pre.size}, max error GPU {g:.2e} m, oracle+ulp {u:.2e} m")
+    assert g <= abs_tol
+    assert g <= PRE_EVENT_ULP_RATIO * u
+    if ids_equal is not None:
+        assert ids_equal[pre].all()
+
+
+def test_event_onset_parity_push_ee():
+    """Until the oracle's discrete state first changes (a contact appears or
+    breaks, an arm joint-limit row switches: po_env.event_sig), the dynamics
+    are smooth and the fp32 GPU path tracks the fp64 oracle to rounding:
+    ee and object positions on every pre-event env-step of a 200-step free
+    run (ee control, 64 envs), with the GPU's contact-cache ids equal to the
+    oracle's (core.py:280-289, panda.py:72-92).  Push blocks the gripper: its
+    fingers rest on their stop with the motor target at the stop, so their
+    limit row's on/off flicker (decided at the 1e-22 level) is not an event
+    here (the PickAndPlace test below excludes it by construction)."""
+    err_gpu, err_ulp, event, fevent, ids_equal = _free_run("push", "ee")
+    _report("push", "ee", err_gpu, err_ulp, event)
+    _check_pre_event("push ee", err_gpu, err_ulp, ~event, 1e-5, ids_equal)
+
+
+def test_event_onset_parity_pick_and_place_ee():
+    """PickAndPlace (free gripper) with the fingers held half open (gripper
+    action 0, both fingers 0.02 m from their limits), so the finger-limit
+    branches that make PickAndPlace chaotic at fp32 resolution
+    cannot occur; events are then contacts and any joint-limit row.  With a
+    random gripper action the first finger-limit change falls on step 0 for
+    nearly every env (reported, not asserted)."""
+    err_gpu, err_ulp, event, fevent, ids_equal = _free_run("pick_and_place", "ee", open_gripper=True)
+    _report("pick_and_place", "ee (gripper open, held)", err_gpu, err_ulp, event | fevent)
+    _check_pre_event("pick_and_place ee (gripper held open)", err_gpu, err_ulp, ~(event | fevent), 1e-5, ids_equal)
+    e2 = _free_run("pick_and_place", "ee")
+    _report("pick_and_place", "ee (random gripper; finger-limit changes are events)", e2[0], e2[1], e2[2] | e2[3])
+
+
+@pytest.mark.parametrize("task,control", [("push", "ee"), ("pick_and_place", "ee"), ("reach", "joints"),
+                                          ("push", "joints")])
+def test_free_running_200_steps(task, control):
+    """The north star's horizon: 200 free-running steps, 64 envs.  After the
+    first contact or joint-limit event the trajectories are chaotic (a finger
+    at its limit flips branch at the 1e-22 level), so the
+    fraction of env-steps within 1e-3 m of the oracle is held (a) to an
+    absolute floor per task and (b) against the oracle's own conditioning at
+    fp32 resolution: an oracle run perturbed by ULP_NOISE every substep.  The
+    GPU (thousands of fp32 roundings per substep) may drift further than one
+    ulp of noise does, by at most 10 points of the fraction."""
+    err_gpu, err_ulp, event, _, _ = _free_run(task, control)
+    frac, frac_ulp = _report(task, control, err_gpu, err_ulp, event)
+    assert frac >= FREE_RUN_FLOOR[(task, control)]
+    assert frac >= frac_ulp - 0.02
+
+
+def test_event_onset_parity_at_bench_config():
+    """The bench workload (PandaPush-v3, 65 536 envs, ee, autoreset, seeds
+    12345 + i, the bench's action stream) for 100 steps, 64 sampled envs
+    stepped alongside by the oracle (autoreset too): on every env-step before
+    the env's first event of an episode (reset starts a new event-free span)
+    ee and object positions agree to rounding (_check_pre_event: 5e-5 m, the
+    spans are up to an episode long, and 2 x an oracle perturbed at fp32
+    resolution)."""
+    B, T = 65536, 100
+    env = make_env("push", "ee", B, autoreset=True)
+    env.reset(seed=(12345 + np.arange(B)).astype(np.uint64))
+    cfg = oracle_config_for(env.sim.cfg)
+    sample = np.linspace(0, B - 1, 64).astype(int)
+    snap = snapshot(env.sim)
+    ref = [oracle_env_from(cfg, snap, int(i)) for i in sample]
+    pert = [oracle_env_from(cfg, snap, int(i)) for i in sample]
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0xC0FFEE)
+    actions = torch.rand(T, B, 3, device="cuda", generator=g) * 2 - 1
+    _, idx = _obs_index("push")
+    err_gpu = np.zeros((T, len(ref)))
+    err_ulp = np.zeros((T, len(ref)))
+    pre = np.zeros((T, len(ref)), bool)
+    resets = 0
+    for s in range(T):
+        obs, r, te, tr, info = env.step(actions[s])
+        og = obs["observation"][torch.from_numpy(sample).cuda()].cpu().numpy()
+        a = actions[s][torch.from_numpy(sample).cuda()].cpu().numpy()
+        for j, e in enumerate(ref):
+            o, ag, dg, rr, t_e, t_r = O.step(cfg, e, a[j], autoreset=True)
+            O.set_state_noise(ULP_NOISE, seed=(s * len(ref) + j) * 2 + 1)
+            op, *_ = O.step(cfg, pert[j], a[j], autoreset=True)
+            O.set_state_noise(0.0)
+            pre[s, j] = e.event_changes == 0
+            err_gpu[s, j] = np.abs(og[j, idx] - o[idx]).max()
+            err_ulp[s, j] = np.abs(op[idx] - o[idx]).max()
+            if t_e or t_r:
+                # the reset starts a new event-free span (both runs reset to
+                # the same state: the reset draws are bit-exact)
+                e.event_changes, e.event_sig = 0, 0
+                pert[j] = copy.deepcopy(e)
+                resets += 1
+    print(f"bench config: {resets} resets")
+    assert resets >= len(ref)
+    _check_pre_event("bench config (PandaPush-v3 x65536, 64 sampled envs, 100 steps)", err_gpu, err_ulp, pre, 5e-5)
 
 
 def test_reach_at_config_size():

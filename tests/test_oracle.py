@@ -337,3 +337,58 @@ def test_finger_limit_branch_sensitivity():
     overshoot = [min(q[7], q[8]) < -5e-3 for q, _ in runs[0][0]], [min(q[7], q[8]) < -5e-3 for q, _ in runs[1][0]]
     assert any(overshoot[0]) or any(overshoot[1])
     assert overshoot[0] != overshoot[1]
+
+
+def test_event_signature_tracks_contact_and_limit_changes():
+    """po_env.event_sig (test bookkeeping for the event-onset parity tests):
+    unchanged while the discrete state is (a cube resting on the table, the
+    arm in free motion), counted once a contact appears (a box dropped onto
+    the table) and it is part of no physics (same trajectory with and
+    without reading it)."""
+    cfg = O.config("push")
+    env = O.new_env(cfg)
+    O.reset(cfg, env, seed=4)
+    O.step(cfg, env, np.zeros(3, np.float32))
+    assert env.event_sig >> 63 == 1 and env.event_changes == 0  # resting cube: 4 ground contacts
+    # lift the cube 5 cm and let it fall: the ground contacts break, then re-form
+    env.obj[0].pos[2] += 0.05
+    for _ in range(10):
+        O.step(cfg, env, np.zeros(3, np.float32))
+    assert env.event_changes >= 2
+    # a joint-limit row appearing is an event: drive joint 0 to its upper limit
+    jc = O.config("reach", control="joints")
+    e = O.new_env(jc)
+    O.reset(jc, e, seed=0)
+    O.step(jc, e, np.zeros(7, np.float32))
+    base = e.event_changes
+    e.q[0] = 2.9671 + 1e-3  # joint 0 upper limit (panda_model.h PM_DOF_TABLE)
+    O.step(jc, e, np.zeros(7, np.float32))
+    assert e.event_changes > base and e.event_kinds & 2
+    assert env.event_kinds & 1  # the cube's ground contacts changed above
+
+
+def test_state_noise_hook_moves_state_by_fp32_ulps():
+    """po_set_state_noise: every state component moves by at most `ulps`
+    fp32 ulps per substep and the hook is off at 0 (bit-equal to no hook)."""
+    cfg = O.config("push")
+    a = np.array([0.2, -0.1, 0.3], np.float32)
+    e0, e1, e2 = O.new_env(cfg), O.new_env(cfg), O.new_env(cfg)
+    for e in (e0, e1, e2):
+        O.reset(cfg, e, seed=9)
+    O.sim_step(cfg, e0)
+    O.set_state_noise(0.0)
+    O.sim_step(cfg, e1)
+    assert np.array_equal(np.array(e0.q), np.array(e1.q)) and np.array_equal(np.array(e0.qd), np.array(e1.qd))
+    O.set_state_noise(1.0, seed=3)
+    try:
+        O.lib().po_substep(O.C.byref(cfg), O.C.byref(e2), None)
+    finally:
+        O.set_state_noise(0.0)
+    e3 = O.new_env(cfg)
+    O.reset(cfg, e3, seed=9)
+    O.lib().po_substep(O.C.byref(cfg), O.C.byref(e3), None)
+    for x, y in ((e2.q, e3.q), (e2.qd, e3.qd), (e2.obj[0].pos, e3.obj[0].pos)):
+        x, y = np.array(x), np.array(y)
+        ulp = np.spacing(np.abs(y).astype(np.float32)).astype(np.float64)
+        assert np.all(np.abs(x - y) <= ulp * 1.0000001)
+        assert np.any(x != y)
