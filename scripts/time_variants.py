@@ -7,7 +7,8 @@ sys.path.insert(0, os.path.join(os.environ["ROOT"], "panda-lang-manip_amd"))
 import pandasim
 out = {}
 for task in os.environ.get("TASKS", "push").split(","):
-    env_id = {"reach": "PandaReach-v3", "push": "PandaPush-v3", "pick_and_place": "PandaPickAndPlace-v3"}[task]
+    env_id = {"reach": "PandaReach-v3", "push": "PandaPush-v3", "pick_and_place": "PandaPickAndPlace-v3",
+              "stack": "PandaStack-v3", "flip": "PandaFlip-v3", "slide": "PandaSlide-v3"}[task]
     B = int(os.environ.get("B", "65536"))
     env = pandasim.make(env_id, num_envs=B)
     env.reset(seed=12345)
