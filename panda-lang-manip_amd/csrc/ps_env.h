@@ -51,6 +51,17 @@ PS_DECLARE_STEP_LAUNCHER(0, 0) PS_DECLARE_STEP_LAUNCHER(0, 1) PS_DECLARE_STEP_LA
 PS_DECLARE_STEP_LAUNCHER(1, 1) PS_DECLARE_STEP_LAUNCHER(2, 0) PS_DECLARE_STEP_LAUNCHER(2, 1)
 PS_DECLARE_STEP_LAUNCHER(3, 0) PS_DECLARE_STEP_LAUNCHER(3, 1) PS_DECLARE_STEP_LAUNCHER(4, 0)
 PS_DECLARE_STEP_LAUNCHER(4, 1) PS_DECLARE_STEP_LAUNCHER(5, 0) PS_DECLARE_STEP_LAUNCHER(5, 1)
+// the 16- and 8-lane group kernels of a pair (not Stack) live in an object of
+// their own (step_kernels.hip with -DPS_STEP_GROUPS=1), called by the pair's
+// launcher
+#define PS_STEP_GROUP_LAUNCHER_NAME_(T, C) ps_launch_step_groups_##T##_##C
+#define PS_STEP_GROUP_LAUNCHER_NAME(T, C) PS_STEP_GROUP_LAUNCHER_NAME_(T, C)
+#define PS_DECLARE_STEP_GROUP_LAUNCHER(T, C) \
+    int PS_STEP_GROUP_LAUNCHER_NAME(T, C)(ps_ctx * c, const void *params, const ps_step_io &io, int lanes, hipStream_t st);
+PS_DECLARE_STEP_GROUP_LAUNCHER(0, 0) PS_DECLARE_STEP_GROUP_LAUNCHER(0, 1) PS_DECLARE_STEP_GROUP_LAUNCHER(1, 0)
+PS_DECLARE_STEP_GROUP_LAUNCHER(1, 1) PS_DECLARE_STEP_GROUP_LAUNCHER(2, 0) PS_DECLARE_STEP_GROUP_LAUNCHER(2, 1)
+PS_DECLARE_STEP_GROUP_LAUNCHER(3, 0) PS_DECLARE_STEP_GROUP_LAUNCHER(3, 1) PS_DECLARE_STEP_GROUP_LAUNCHER(5, 0)
+PS_DECLARE_STEP_GROUP_LAUNCHER(5, 1)
 #define PS_SIM_LAUNCHER_NAME_(NOBJ, SHAPE) ps_launch_sim_step_##NOBJ##_##SHAPE
 #define PS_SIM_LAUNCHER_NAME(NOBJ, SHAPE) PS_SIM_LAUNCHER_NAME_(NOBJ, SHAPE)
 #define PS_DECLARE_SIM_LAUNCHER(NOBJ, SHAPE) \

@@ -790,6 +790,8 @@ PS_D int box_box(const Scene &sc, const Body &b0, const Body &b1, const M3 &R0, 
 //   contact rows  |dl| - sqrt(1e-7) dinv
 //   joint rows    |dl| den - sqrt(1e-7)      (den = M^-1_dd, in registers)
 constexpr float kResidualAbs = 3.16227766e-4f;
+
+
 // A row-family gate with a layout hint of how often it is open (the cube's
 // ground rows and gripper slots 0-1: open; slots 2-3 and joint limits:
 // closed).  A lone wave pays ~20 cycles for a taken branch (the instruction
@@ -1044,11 +1046,17 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         for (int k = 0; k < K; k++) dvm[k] = fmaf(M[2][k], dlb, fmaf(M[1][k], dla, dvm[k]));
         res = fmaxf(res, fmaxf(row_viol(dla, dinv[1]), row_viol(dlb, dinv[2])));
     };
-    auto contacts = [&]() {
+    // the object's ground normals touch only object DoFs: they commute with
+    // the joint rows (robot DoFs only), so they run in the motor rows' block,
+    // ungated (a slot a lane lacks is an all-zero no-op), where their
+    // dependent chains interleave with the motor rows'
+    auto ground_normals = [&]() {
+        if constexpr (NOBJ > 0) {
 #pragma unroll
-        for (int c = 0; c < NG; c++)
-            if (NOBJ > 0 && (gate_gnd & (1u << c)))
-                normal(gJ[c][0], gM[c][0], gc[c].rhs[0], gc[c].dinv[0], gc[c].lam[0]);
+            for (int c = 0; c < NG; c++) normal(gJ[c][0], gM[c][0], gc[c].rhs[0], gc[c].dinv[0], gc[c].lam[0]);
+        }
+    };
+    auto contacts = [&]() {
 #pragma unroll
         for (int c = 0; c < NR; c++)
             if (gate_robot & (1u << c)) normal(rJ[c][0], rM[c][0], rc[c].rhs[0], rc[c].dinv[0], rc[c].lam[0]);
@@ -1065,6 +1073,7 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
 #endif
         res = 0.0f;
         down(motor_row);
+        ground_normals();
         if (gate_lim != 0u) down(limit_row);
         contacts();
         if (res <= 0.0f) break;
@@ -1074,6 +1083,7 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         res = 0.0f;
         if (gate_lim != 0u) up(limit_row);
         up(motor_row);
+        ground_normals();
         contacts();
         if (res <= 0.0f) break;
     }
@@ -1689,9 +1699,12 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             }
     }
 
-    auto contacts = [&]() {
-        // normals: ground contacts, pair contacts, then gripper contacts.
-        // Stack: the pair rows' read-only data come from the global stash
+    auto object_normals = [&]() {
+        if constexpr (NOBJ == 2) {
+        // Stack: the cubes' ground normals and the pair normals touch only
+        // the cubes' DoFs, so they commute with the joint rows and run right
+        // after the motor rows, ungated for the ground (a slot a lane lacks
+        // has 1/den = 0: an exact no-op).  The pair rows' read-only data come from the global stash
         // (PAIR_FLOATS).  Every slot's loads are issued here, before the
         // ground rows, so their L2 latency runs under those rows and the wave
         // waits once per sweep, not once per contact (unused slots hold
@@ -1717,8 +1730,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         for (int b = 0; b < NOBJ; b++) {
             const float inv_m = od[b].inv_m;
 #pragma unroll
-            for (int c = 0; c < NG; c++)
-                if (PS_GATE(gate_ground[b] & (1u << c), 1)) {
+            for (int c = 0; c < NG; c++) {
                     GroundContact &g = gc[b][c];
                     V3 gr = g.r;
                     float grhs = g.rhs[0], gdinv = g.dinv[0];
@@ -1769,6 +1781,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     }
             }
         }
+        }
+    };
+    auto contacts = [&]() {
+        // normals: the gripper contacts (the objects' ground and pair
+        // normals ran with the motor rows: ground_normals, object_normals)
 #pragma unroll
         for (int c = 0; c < NR; c++)
             if (PS_GATE(gate_robot & (1u << c), c < 2)) {
@@ -1970,6 +1987,33 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             }
     };
 
+    // One object (not Stack): its ground normals touch only the object's
+    // DoFs and commute with the joint rows, so they run ungated in the motor
+    // rows' block (a slot a lane lacks is an all-zero no-op) -- Bullet's
+    // order up to commuting rows
+    auto ground_normals = [&]() {
+        if constexpr (NOBJ == 1) {
+#pragma unroll
+            for (int c = 0; c < NG; c++) {
+                GroundContact &g = gc[0][c];
+                const V3 rn = mk(g.r.y, -g.r.x, 0.0f);  // r x (0,0,1)
+                float dl = g.rhs[0] - g.dinv[0] * (rn.x * dw[0].x + rn.y * dw[0].y + dvl[0].z);
+                const float nl = fminf(fmaxf(g.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
+                dl = nl - g.lam[0];
+                g.lam[0] = nl;
+                if constexpr (ANISO) {
+                    dw[0] = dw[0] + od[0].inv_inertia(mk(rn.x * dl, rn.y * dl, 0.0f));
+                } else {
+                    const float dI = dl * od[0].iI;
+                    dw[0].x = fmaf(rn.x, dI, dw[0].x);
+                    dw[0].y = fmaf(rn.y, dI, dw[0].y);
+                }
+                dvl[0].z = fmaf(dl, od[0].inv_m, dvl[0].z);
+                res = fmaxf(res, row_viol(dl, g.dinv[0]));
+            }
+        }
+    };
+
     // btSequentialImpulseConstraintSolver alternates the order of the
     // non-contact rows by iteration parity: even iterations run them in
     // reverse (motors 8..0, then limits 8..0), odd ones forward (limits 0..8,
@@ -1981,6 +2025,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         res = 0.0f;
 #pragma unroll
         for (int d = 8; d >= 0; d--) motor_row(d);
+        ground_normals();
+        object_normals();
         if (PS_GATE(gate_lim != 0u, 0)) {
 #pragma unroll
             for (int d = 8; d >= 0; d--) limit_row(d);
@@ -1996,6 +2042,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         }
 #pragma unroll
         for (int d = 0; d < 9; d++) motor_row(d);
+        ground_normals();
+        object_normals();
         contacts();
         if (res <= 0.0f) break;
     }

@@ -19,6 +19,10 @@ VARIANTS = {
     # IEEE mode off: drops the v_max x,x,x canonicalisations before min/max
     # (68 of ~3000 instructions in the Push PGS loop); NaN handling only
     "ieee_off": ["-fno-honor-nans", "-mno-amdgpu-ieee"],
+    # group-kernel miscompute bisection
+    "o1": ["-O1"],
+    "prealloc": ["-mllvm", "-amdgpu-prealloc-sgpr-spill-vgprs=1"],
+    "nodppc": ["-mllvm", "-amdgpu-dpp-combine=0"],
 }
 
 

@@ -614,3 +614,31 @@ def test_ragged_batch_parity(ps, B, lanes):
             o, *_ = O.step(cfg, oracle_env_from(cfg, snap, i), a[i])
             for k, idx in groups.items():
                 assert np.abs(og[i, idx] - o[idx]).max() <= TOL["push"][k], (B, i, k)
+
+
+GROUP_TASKS = [(t, c) for t, c in TASKS if t != "stack"]
+
+
+@pytest.mark.parametrize("task,control", GROUP_TASKS)
+def test_group_kernels_match_one_lane(ps, task, control):
+    """The 16- and 8-lane group kernels against the one-lane kernel over the
+    same step from the same reset (the joint rows q, qd).  They run the same
+    rows in the same order; the group sums round differently and Slide's group
+    kernels are built at -O1 (build.py), so they agree to fp32 rounding
+    amplified by one step of PGS: 1.5e-4 at most on the MI355X (profiles/
+    r03c_group_vs_one_lane.log).  The miscompiled -O3 Slide group kernels this
+    guards against were off by 6.8e-3 to 2.1e-1."""
+    B = 64
+    res = {}
+    for lanes in (1, 8, 16):
+        env = make_env(ps, task, control, B, lanes=lanes)
+        assert env.lanes_per_env == lanes
+        env.autoreset = False
+        env.reset(seed=12345)
+        a = np.random.default_rng(7).uniform(-1, 1, size=(B, env.action_dim)).astype(np.float32)
+        env.step(torch.from_numpy(a).cuda())
+        res[lanes] = env.sim.f[0:18, :B].double().cpu().numpy()
+    for lanes in (8, 16):
+        err = np.abs(res[lanes] - res[1]).max()
+        print(f"{task} {control} {lanes} lanes vs 1: {err:.1e}")
+        assert err < 2e-3, (lanes, err)
