@@ -381,6 +381,13 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             work, out["cpu_baseline"] = cpu_baseline(spec["task"], args.cpu_seconds)
             out["roofline"]["fp32"] = fp32_roofline(work, env.sim.cfg.n_objects, value / world)
+            ex = out["roofline"].get("fp32_executed")
+            if ex:
+                # executed (PMC) over algorithmic FLOPs per launch: the share of
+                # issue spent on lanes whose env has already converged, gated
+                # rows a lane lacks, and the like
+                algo = out["roofline"]["fp32"]["flops_per_env_step"] * B
+                ex["executed_over_algorithmic"] = round(ex["flops_per_launch"] / algo, 3)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

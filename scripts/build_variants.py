@@ -26,17 +26,27 @@ VARIANTS = {
 }
 
 
+# variants that change the per-unit flags of build.UNITS instead
+UNIT_VARIANTS = {
+    # the group-kernel objects at the library's -O3 (the product builds them at
+    # -O1)
+    "groups_o3": lambda units: [(n, s, [d for d in defs if d != "-O1"]) for n, s, defs in units],
+}
+
+
 def main(names):
     out_dir = os.path.join(ROOT, "scripts", "bin", "variants")
     os.makedirs(out_dir, exist_ok=True)
+    product_units = list(B.UNITS)
     for n in names:
         out = os.path.join(out_dir, f"lib_{n}.so")
+        B.UNITS = UNIT_VARIANTS[n](product_units) if n in UNIT_VARIANTS else product_units
         try:
-            B.build(variant="", extra=VARIANTS[n], out=out, verbose=False)
+            B.build(variant="", extra=VARIANTS.get(n, []), out=out, verbose=False)
             print(n, "ok")
         except Exception as e:  # a variant that does not compile is reported, not fatal
             print(n, "failed:", e)
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or list(VARIANTS))
+    main(sys.argv[1:] or list(VARIANTS) + list(UNIT_VARIANTS))

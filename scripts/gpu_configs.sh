@@ -6,9 +6,11 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for cfg in ${CONFIGS:-"PandaReach-v3:4096 PandaReachJoints-v3:4096 PandaPush-v3:8192 PandaPickAndPlace-v3:8192 \
-           PandaPush-v3:65536 PandaReachDense-v3:65536 PandaReachJoints-v3:65536 PandaPickAndPlace-v3:65536 \
-           PandaSlide-v3:65536 PandaStack-v3:65536 PandaFlip-v3:65536"}; do
+# (a quoted default inside ${CONFIGS:-"..."} would be one word: one run)
+ALL="PandaReach-v3:4096 PandaReachJoints-v3:4096 PandaPush-v3:8192 PandaPickAndPlace-v3:8192
+     PandaPush-v3:65536 PandaReachDense-v3:65536 PandaReachJoints-v3:65536 PandaPickAndPlace-v3:65536
+     PandaSlide-v3:65536 PandaStack-v3:65536 PandaFlip-v3:65536"
+for cfg in ${CONFIGS:-$ALL}; do
   timeout -k 10 300 python bench.py --no-cpu-baseline --env-id ${cfg%%:*} --batch ${cfg##*:} >> gpurun_out/configs.jsonl 2>>gpurun_out/configs.err || exit $?
 done
 for lanes in $LANES; do
