@@ -1,11 +1,20 @@
 # Group kernels (16 and 8 lanes per env) against the one-lane kernel: q/qd after
 # one step from the same reset, per task and control (diagnostic; the GPU test
 # is tests/test_gpu_parity.py::test_group_kernels_match_one_lane).
-import sys, numpy as np, torch
+# usage: python scripts/group_vs_one_lane.py [task,task,...] [-v]
+import sys
+
+import numpy as np
+import torch
+
 sys.path.insert(0, 'panda-lang-manip_amd')
-from pandasim.envs import PandaVecEnv
+from pandasim.envs import PandaVecEnv  # noqa: E402
+
 B = 64
-for task in ("slide", "push", "pick_and_place", "reach"):
+tasks = [a for a in sys.argv[1:] if not a.startswith("-")]
+tasks = tasks[0].split(",") if tasks else ["slide", "push", "pick_and_place", "reach", "flip"]
+verbose = "-v" in sys.argv
+for task in tasks:
     for control in ("joints", "ee"):
         res = {}
         for lanes in (1, 8, 16):
@@ -15,6 +24,16 @@ for task in ("slide", "push", "pick_and_place", "reach"):
             rng = np.random.default_rng(7)
             a = rng.uniform(-1, 1, size=(B, env.action_dim)).astype(np.float32)
             env.step(torch.from_numpy(a).cuda())
-            res[lanes] = env.sim.f[0:18, :B].double().cpu().numpy()
+            res[lanes] = env.sim.f[:, :B].double().cpu().numpy()
+        d8, d16 = np.abs(res[8] - res[1]), np.abs(res[16] - res[1])
         print(task, control, "q/qd max diff vs 1 lane: 8 lanes %.1e, 16 lanes %.1e" % (
-            np.abs(res[8] - res[1]).max(), np.abs(res[16] - res[1]).max()), flush=True)
+            d8[0:18].max(), d16[0:18].max()), flush=True)
+        if verbose:
+            for name, d in (("8", d8), ("16", d16)):
+                rows = np.nonzero(d.max(axis=1) > 0)[0]
+                envs = np.nonzero(d[0:18].max(axis=0) > 1e-3)[0]
+                print(f"   {name} lanes: rows differing {rows.tolist()[:40]}; envs off by > 1e-3 {envs.tolist()[:20]}")
+                for r in rows[:12]:
+                    e = int(np.argmax(d[r]))
+                    print(f"     row {r}: max {d[r].max():.2e} at env {e} (1 lane {res[1][r, e]:.6g}, "
+                          f"{name} lanes {res[int(name)][r, e]:.6g})")
