@@ -10,7 +10,7 @@ The group kernels are compiled at -O1: at -O2/-O3 this compiler miscomputed
 Slide's (joint velocities off by up to 0.2 rad/s after one
 step; which kernel depended on unrelated edits and -mllvm options, and one
 experiment broke Push's 8-lane kernel the same way), while at -O1 every group
-kernel matches its one-lane kernel (tests/test_gpu_parity.py::
+kernel agrees with its one-lane kernel to fp32 rounding (tests/test_gpu_parity.py::
 test_group_kernels_match_one_lane) and runs as fast or faster (Push and
 PickAndPlace at 8 192 envs: 2.17 -> 2.07 ms per step).
 

@@ -168,6 +168,12 @@ def test_reset_places_objects_at_rest(task):
 # (oracle.set_state_noise).  A second oracle run with this noise shows how far
 # two runs that differ only by fp32 rounding of the state drift apart.
 ULP_NOISE = 1.0
+# After the first event the runs are chaotic, and which env leaves the 1e-3 band
+# first is a coin flip between two runs that differ by rounding (one env of 64
+# is 1.6 points of the fraction): the yardstick is an ensemble of ULP_RUNS
+# perturbed oracle runs (independent noise), and the GPU's fraction is held to
+# the ensemble's lowest less 2 points.
+ULP_RUNS = 3
 # Free-run floors (absolute, next to the relative yardstick): fraction of
 # env-steps whose ee/object positions are within 1e-3 m of the oracle, 64 envs
 # x 200 steps, seed 2024.  Measured in profiles/r03*_pytest_gpu.log.
@@ -203,11 +209,11 @@ def _free_run(task, control, B=64, T=200, seed=2024, open_gripper=False):
     cfg = oracle_config_for(env.sim.cfg)
     snap = snapshot(env.sim)
     ref = [oracle_env_from(cfg, snap, i) for i in range(B)]
-    pert = [oracle_env_from(cfg, snap, i) for i in range(B)]
+    pert = [[oracle_env_from(cfg, snap, i) for i in range(B)] for _ in range(ULP_RUNS)]
     rng = np.random.default_rng(seed)
     nobj, idx = _obs_index(task)
     err_gpu = np.zeros((T, B))
-    err_ulp = np.zeros((T, B))
+    err_ulp = np.zeros((ULP_RUNS, T, B))
     event = np.zeros((T, B), bool)
     fevent = np.zeros((T, B), bool)
     kinds = np.zeros((T, B), np.int8)
@@ -228,10 +234,11 @@ def _free_run(task, control, B=64, T=200, seed=2024, open_gripper=False):
             gc, oc = gpu_cache(f, i), oracle_cache(ref[i])
             ids_equal[s, i] = all([k for k, _ in gc[g]] == [k for k, _ in oc[g]] for g in ("ground0", "ground1", "robot")) \
                 and len(gc["pair"]) == len(oc["pair"])
-            O.set_state_noise(ULP_NOISE, seed=(s * B + i) * 2 + 1)
-            op, *_ = O.step(cfg, pert[i], a[i])
-            O.set_state_noise(0.0)
-            err_ulp[s, i] = np.abs(op[idx] - o[idx]).max()
+            for k in range(ULP_RUNS):
+                O.set_state_noise(ULP_NOISE, seed=((s * B + i) * 2 + 1) + k * 1000003)
+                op, *_ = O.step(cfg, pert[k][i], a[i])
+                O.set_state_noise(0.0)
+                err_ulp[k, s, i] = np.abs(op[idx] - o[idx]).max()
     _RUNS[key] = (err_gpu, err_ulp, event, fevent, ids_equal)
     os.makedirs("gpurun_out", exist_ok=True)
     np.savez_compressed(f"gpurun_out/free_run_{task}_{control}{'_open' if open_gripper else ''}.npz", err_gpu=err_gpu,
@@ -240,15 +247,18 @@ def _free_run(task, control, B=64, T=200, seed=2024, open_gripper=False):
 
 
 def _report(task, control, err_gpu, err_ulp, event):
+    """err_ulp: [ULP_RUNS, T, B]; returns the GPU's fraction within 1e-3 and
+    the lowest fraction of the perturbed oracle runs."""
     pre = ~event
-    frac, frac_ulp = float((err_gpu <= 1e-3).mean()), float((err_ulp <= 1e-3).mean())
+    frac = float((err_gpu <= 1e-3).mean())
+    fracs = [float((e <= 1e-3).mean()) for e in err_ulp]
     first = np.where(event.any(0), event.argmax(0), event.shape[0])
     print(f"{task} {control}: GPU within 1e-3 of the oracle in {frac * 100:.2f} % of env-steps (worst "
-          f"{err_gpu.max():.1e} m); oracle + {ULP_NOISE:g} fp32 ulp/substep noise: {frac_ulp * 100:.2f} % "
-          f"(worst {err_ulp.max():.1e}); pre-event env-steps {int(pre.sum())} / {pre.size} (first event: median step "
-          f"{int(np.median(first))}), pre-event max error GPU {err_gpu[pre].max() if pre.any() else 0:.2e} m, "
-          f"oracle+ulp {err_ulp[pre].max() if pre.any() else 0:.2e} m")
-    return frac, frac_ulp
+          f"{err_gpu.max():.1e} m); oracle + {ULP_NOISE:g} fp32 ulp/substep noise, {len(fracs)} runs: "
+          f"{', '.join(f'{f * 100:.2f}' for f in fracs)} % (worst {err_ulp.max():.1e}); pre-event env-steps "
+          f"{int(pre.sum())} / {pre.size} (first event: median step {int(np.median(first))}), pre-event max error "
+          f"GPU {err_gpu[pre].max() if pre.any() else 0:.2e} m, oracle+ulp {err_ulp[0][pre].max() if pre.any() else 0:.2e} m")
+    return frac, min(fracs)
 
 
 # Pre-event bound: until the first event the only difference between the
@@ -286,7 +296,7 @@ def test_event_onset_parity_push_ee():
     here (the PickAndPlace test below excludes it by construction)."""
     err_gpu, err_ulp, event, fevent, ids_equal = _free_run("push", "ee")
     _report("push", "ee", err_gpu, err_ulp, event)
-    _check_pre_event("push ee", err_gpu, err_ulp, ~event, 1e-5, ids_equal)
+    _check_pre_event("push ee", err_gpu, err_ulp[0], ~event, 1e-5, ids_equal)
 
 
 def test_event_onset_parity_pick_and_place_ee():
@@ -298,7 +308,7 @@ def test_event_onset_parity_pick_and_place_ee():
     nearly every env (reported, not asserted)."""
     err_gpu, err_ulp, event, fevent, ids_equal = _free_run("pick_and_place", "ee", open_gripper=True)
     _report("pick_and_place", "ee (gripper open, held)", err_gpu, err_ulp, event | fevent)
-    _check_pre_event("pick_and_place ee (gripper held open)", err_gpu, err_ulp, ~(event | fevent), 1e-5, ids_equal)
+    _check_pre_event("pick_and_place ee (gripper held open)", err_gpu, err_ulp[0], ~(event | fevent), 1e-5, ids_equal)
     e2 = _free_run("pick_and_place", "ee")
     _report("pick_and_place", "ee (random gripper; finger-limit changes are events)", e2[0], e2[1], e2[2] | e2[3])
 
@@ -311,9 +321,8 @@ def test_free_running_200_steps(task, control):
     at its limit flips branch at the 1e-22 level), so the
     fraction of env-steps within 1e-3 m of the oracle is held (a) to an
     absolute floor per task and (b) against the oracle's own conditioning at
-    fp32 resolution: an oracle run perturbed by ULP_NOISE every substep.  The
-    GPU (thousands of fp32 roundings per substep) may drift further than one
-    ulp of noise does, by at most 10 points of the fraction."""
+    fp32 resolution: ULP_RUNS oracle runs perturbed by ULP_NOISE every
+    substep, whose lowest fraction the GPU must reach less 2 points."""
     err_gpu, err_ulp, event, _, _ = _free_run(task, control)
     frac, frac_ulp = _report(task, control, err_gpu, err_ulp, event)
     assert frac >= FREE_RUN_FLOOR[(task, control)]
