@@ -17,7 +17,7 @@ BATCH=${BATCH:-65536}
 P="--output-format csv -o run"
 BENCH="$R/bench.py --steps 100 --warmup 10 --no-cpu-baseline --env-id $ENV_ID --batch $BATCH"
 has() { case " $STAGES " in *" $1 "*) return 0;; esac; return 1; }
-run() { echo "[gpu_round] $*"; "$@" || { rc=$?; echo "[gpu_round] failed rc=$rc: $*"; exit $rc; }; }
+run() { echo "[gpu_round] $*" >&2; "$@" || { rc=$?; echo "[gpu_round] failed rc=$rc: $*"; exit $rc; }; }
 if has tests; then
   run timeout -k 10 900 python -u -m pytest tests -x -q -m gpu -rf --timeout 120 --timeout-method thread \
       ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1
@@ -40,7 +40,8 @@ if has pmc; then
 fi
 cd $R
 if has phase; then
-  for id in ${PHASE_IDS:-"PandaPush-v3:65536 PandaStack-v3:65536"}; do
+  DEFAULT_IDS="PandaPush-v3:65536 PandaStack-v3:65536"  # (a quoted default inside ${:-} is one word)
+  for id in ${PHASE_IDS:-$DEFAULT_IDS}; do
     run timeout -k 10 300 python scripts/phase_profile.py ${id%%:*} ${id##*:} 20 >> gpurun_out/phase.log 2>&1
   done
 fi

@@ -100,8 +100,10 @@ def main():
             acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
         for k, cs in acc.items():
             extra[k] = {c: sum(v) / len(v) for c, v in cs.items()}
-    fpath = os.path.join(OUT, f"{args.prefix}_flops", "run_counter_collection.csv")
-    if os.path.exists(fpath):
+    # the FP32 instruction pass (scripts/gpu_round.sh writes prof_fp32; older rounds prof_flops)
+    fpaths = [os.path.join(OUT, f"{args.prefix}_{sub}", "run_counter_collection.csv") for sub in ("fp32", "flops")]
+    fpath = next((f for f in fpaths if os.path.exists(f)), None)
+    if fpath:
         acc = collections.defaultdict(lambda: collections.defaultdict(list))
         for r in csv.DictReader(open(fpath)):
             acc[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
