@@ -3,6 +3,7 @@ draw order, goal arithmetic, distance, reward and success against the
 reference task goldens, with a recording stand-in for PandaSim whose per-env
 generators are numpy's own PCG64 (the device kernels are covered by the -m gpu
 tests)."""
+import os
 import numpy as np
 import pytest
 import torch
@@ -145,3 +146,37 @@ def test_time_limit_wrapper():
     assert env.step(None)[3].all()
     env.reset()
     assert not env.step(None)[3].any()
+
+
+def _model_header():
+    with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                           "panda_model.h")) as f:
+        return f.read()
+
+
+def test_finger_pad_proxies_sit_on_the_pads():
+    """The finger collision proxies (PM_SPHERE_TABLE: two spheres per finger,
+    the meshes being unavailable) against an independent source in the
+    reference: contact-graspnet's Panda gripper control points
+    (panda_gym/envs/contact_graspnet/gripper_control_points/panda.npy, 20
+    points in the hand frame) put the finger pads at z = 0.0753 .. 0.1053 m
+    from the hand origin and 0.0527 m either side of the centre line with the
+    gripper fully open.  The sphere centres must lie on that pad band (hand
+    z), and with the fingers fully open (0.04 m each) within a sphere radius
+    of the pad's lateral position."""
+    import re
+    h = _model_header()
+    # finger joint origin z in the hand frame (links 9 and 10: PM_JOINT_PRISMATIC rows)
+    fz = [float(m.group(1)) for m in re.finditer(
+        r"X\((?:9|10), 8, PM_JOINT_PRISMATIC, 0\.0, 0\.0, ([0-9.]+)", h)]
+    assert len(fz) == 2 and fz[0] == fz[1]
+    spheres = [tuple(float(v) for v in m.groups()) for m in re.finditer(
+        r"X\((9|10), ([-0-9.]+), ([-0-9.]+), ([-0-9.]+), ([0-9.]+), ([0-9.]+)\)", h)]
+    assert len(spheres) == 4
+    pad_z, pad_y_open, q_open = (0.0753, 0.1053), 0.0527, 0.04
+    for link, cx, cy, cz, r, mu in spheres:
+        z = fz[0] + cz
+        assert pad_z[0] <= z <= pad_z[1], (link, z)
+        y_open = abs(cy) + q_open  # finger frame y plus the prismatic opening, hand frame
+        assert abs(y_open - pad_y_open) <= r, (link, y_open)
+        assert mu == 1.0  # panda.py:47-48
