@@ -2023,6 +2023,16 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         PS_COUNT_IT();
         L = lds.opaque();
         res = 0.0f;
+        // one object: M^-1 enters each iteration pair in VGPRs (an empty asm
+        // with a "v" operand), else the allocator parks it in AGPRs and
+        // every motor row reads its column back (v_accvgpr_read): the PGS
+        // loop's AGPR reads 442 -> 340 per iteration pair, Push 3.03 ->
+        // 3.01 ms (profiles/r03h_variants_pin.log; Reach, no object, got
+        // slower and keeps the allocator's choice)
+        if constexpr (NOBJ == 1) {
+#pragma unroll
+            for (int k = 0; k < 45; k++) asm volatile("" : "+v"(Mi[k]));
+        }
 #pragma unroll
         for (int d = 8; d >= 0; d--) motor_row(d);
         ground_normals();
