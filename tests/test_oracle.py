@@ -392,3 +392,74 @@ def test_state_noise_hook_moves_state_by_fp32_ulps():
         ulp = np.spacing(np.abs(y).astype(np.float32)).astype(np.float64)
         assert np.all(np.abs(x - y) <= ulp * 1.0000001)
         assert np.any(x != y)
+
+
+# ------------------------------------------------------------------------------
+# Lagrangian-mechanics identities.  The oracle's mass matrix is a sum over
+# links of J^T m J + Jw^T I Jw (panda_oracle.c), its bias forces a world-frame
+# recursive Newton-Euler pass, and its link COM positions plain FK: three
+# separate code paths, so these identities pin its dynamics without any
+# PyBullet output (the GPU kernels -- composite-rigid-body M, prefix-sum RNEA --
+# are held to the oracle by tests/test_gpu_parity.py).
+def _link_masses():
+    import re
+    with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include",
+                           "panda_model.h")) as f:
+        h = f.read()
+    body = h[h.index("#define PM_LINK_TABLE(X)"):h.index("/* DoF -> link index")]
+    rows = re.findall(r"X\(([^)]*)\)", body.replace("\\\n", " "))
+    masses = {}
+    for r in rows:
+        f = [x.strip() for x in r.split(",")]
+        if f[0].isdigit():
+            masses[int(f[0])] = float(f[13])
+    return masses
+
+
+def _random_q(rng):
+    lo = np.array([-2.9, -1.7, -2.9, -3.0, -2.9, 0.0, -2.9, 0.0, 0.0])
+    hi = np.array([2.9, 1.7, 2.9, -0.1, 2.9, 3.7, 2.9, 0.04, 0.04])
+    return lo + (hi - lo) * rng.random(9)
+
+
+def test_mass_matrix_is_symmetric_positive_definite():
+    cfg, rng = kat_config(), np.random.default_rng(1)
+    for _ in range(20):
+        M = O.mass_matrix(cfg, _random_q(rng))
+        assert np.allclose(M, M.T, atol=1e-14)
+        assert np.linalg.eigvalsh(M).min() > 0
+
+
+def test_gravity_torque_is_the_potential_gradient():
+    """h(q, 0) = dV/dq with V = sum_i m_i g z_i over the links' COM heights."""
+    cfg, rng = kat_config(), np.random.default_rng(2)
+    masses = _link_masses()
+    assert len(masses) == 12 and all(masses[i] > 0 for i in (0, 1, 2, 3, 4, 5, 6, 8, 9, 10))
+
+    def potential(q):
+        env = O.new_env(cfg)
+        env.q[:] = q
+        return sum(m * 9.81 * O.link_state(cfg, env, link)[0][2] for link, m in masses.items() if m > 0)
+
+    for _ in range(10):
+        q = _random_q(rng)
+        g = O.bias_forces(cfg, q, np.zeros(9))
+        eps = 1e-6
+        grad = np.array([(potential(q + eps * e) - potential(q - eps * e)) / (2 * eps) for e in np.eye(9)])
+        assert np.allclose(g, grad, rtol=1e-6, atol=1e-7), (g, grad)
+
+
+def test_coriolis_terms_follow_from_the_mass_matrix():
+    """The part of h(q, qd) even in qd, less gravity, is C(q, qd) qd with
+    (C qd)_i = sum_jk (dM_ij/dq_k - 1/2 dM_jk/dq_i) qd_j qd_k (Christoffel
+    symbols of M).  btMultiBody's link damping is odd in the velocity
+    (m d (1 + |v|) v), so it cancels in h(q, qd) + h(q, -qd)."""
+    cfg, rng = kat_config(), np.random.default_rng(3)
+    for _ in range(10):
+        q, qd = _random_q(rng), rng.normal(0.0, 1.0, 9)
+        even = 0.5 * (O.bias_forces(cfg, q, qd) + O.bias_forces(cfg, q, -qd)) - O.bias_forces(cfg, q, np.zeros(9))
+        eps = 1e-6
+        dM = np.stack([(O.mass_matrix(cfg, q + eps * e) - O.mass_matrix(cfg, q - eps * e)) / (2 * eps)
+                       for e in np.eye(9)])  # dM[k] = dM/dq_k
+        cqd = np.einsum("kij,j,k->i", dM, qd, qd) - 0.5 * np.einsum("ijk,j,k->i", dM, qd, qd)
+        assert np.allclose(even, cqd, rtol=1e-5, atol=1e-7), (even, cqd)
