@@ -153,29 +153,46 @@ def test_flop_model_counts():
     assert f["flops_per_env_step"] == sum(f["split"].values())
 
 
-def test_build_freshness_is_decided_by_content_not_mtime():
+def test_build_freshness_is_decided_by_content_not_mtime(tmp_path, monkeypatch):
     """build.py's stamp: a header whose bytes change while its mtime does not
-    makes the library stale, and _lib refuses to load a stale library."""
+    makes the library stale, and _lib refuses to load a stale library.  Run
+    on a copy of the sources and the library (the tree itself is never
+    edited, so parallel test workers and an interrupted run are safe)."""
+    import shutil
+
     from pandasim import _lib
     from pandasim import build as B
 
     assert not B.needs_build(), "build the library first (python -m pandasim.build)"
+    root = str(tmp_path)
+    pkg = os.path.relpath(os.path.dirname(B.CSRC), B.ROOT)
+    shutil.copytree(B.CSRC, os.path.join(root, pkg, "csrc"))
+    shutil.copytree(B.INCLUDE, os.path.join(root, "include"))
+    os.makedirs(os.path.join(root, pkg, "pandasim"))
+    out = os.path.join(root, pkg, "pandasim", os.path.basename(B.OUT))
+    shutil.copy(B.OUT, out)
+    shutil.copy(B.stamp_path(B.OUT), B.stamp_path(out))
+    monkeypatch.setattr(B, "FLAGS", [f.replace(B.INCLUDE, os.path.join(root, "include")) for f in B.FLAGS])
+    monkeypatch.setattr(B, "ROOT", root)
+    monkeypatch.setattr(B, "CSRC", os.path.join(root, pkg, "csrc"))
+    monkeypatch.setattr(B, "INCLUDE", os.path.join(root, "include"))
+    monkeypatch.setattr(B, "OUT", out)
+    assert not B.needs_build()  # the copy carries the same stamp
+    _lib.check_fresh(out)
     hdr = os.path.join(B.CSRC, "ps_common.h")
     st = os.stat(hdr)
     orig = open(hdr, "rb").read()
-    try:
-        with open(hdr, "wb") as f:
-            f.write(orig + b"// freshness probe\n")
-        os.utime(hdr, ns=(st.st_atime_ns, st.st_mtime_ns))
-        assert os.stat(hdr).st_mtime_ns == st.st_mtime_ns
-        assert B.needs_build()
-        with pytest.raises(_lib.PandasimError, match="stale"):
-            _lib.check_fresh(B.OUT)
-    finally:
-        with open(hdr, "wb") as f:
-            f.write(orig)
-        os.utime(hdr, ns=(st.st_atime_ns, st.st_mtime_ns))
+    with open(hdr, "wb") as f:
+        f.write(orig + b"// freshness probe\n")
+    os.utime(hdr, ns=(st.st_atime_ns, st.st_mtime_ns))
+    assert os.stat(hdr).st_mtime_ns == st.st_mtime_ns
+    assert B.needs_build()
+    with pytest.raises(_lib.PandasimError, match="stale"):
+        _lib.check_fresh(out)
+    with open(hdr, "wb") as f:
+        f.write(orig)
+    os.utime(hdr, ns=(st.st_atime_ns, st.st_mtime_ns))
     assert not B.needs_build()
-    _lib.check_fresh(B.OUT)
+    _lib.check_fresh(out)
     # flags are part of the stamp too
     assert B.fingerprint("") != B.fingerprint("prof") != B.fingerprint("", ["-DX"])
