@@ -639,9 +639,8 @@ __global__ __launch_bounds__(kBlock, PS_STEP_MIN_WAVES) void k_step(KParams P, c
         lds.goff = StateView::off(i, 4);
         lds.gpair = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_PAIR_OFFSET * s.stride +
                                                                  i * (NP * PAIR_FLOATS));
-        if constexpr (GRIP_FLOATS > 0)
-            lds.ggrip = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_GRIP_OFFSET * s.stride +
-                                                                     i * GRIP_FLOATS);
+        lds.ggrip = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_GRIP_OFFSET * s.stride +
+                                                                 i * GRIP_FLOATS);
     }
     run_substeps<T::NOBJ, T::SHAPE, true, G>(P, i, PM_SUBSTEPS, q, qd, bd, lds, live, tgt PS_PROF_ARG);
     double g[6] = {0, 0, 0, 0, 0, 0};
@@ -725,9 +724,8 @@ __global__ __launch_bounds__(kBlock) void k_sim_step(KParams P, int n_substeps) 
         lds.goff = StateView::off(i, 4);
         lds.gpair = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_PAIR_OFFSET * s.stride +
                                                                  i * (NP * PAIR_FLOATS));
-        if constexpr (GRIP_FLOATS > 0)
-            lds.ggrip = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_GRIP_OFFSET * s.stride +
-                                                                     i * GRIP_FLOATS);
+        lds.ggrip = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_GRIP_OFFSET * s.stride +
+                                                                 i * GRIP_FLOATS);
     }
 #ifdef PS_PROFILE_PHASES
     PhaseTimer pt;

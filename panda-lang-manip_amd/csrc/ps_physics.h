@@ -572,24 +572,16 @@ constexpr int LDS_FLOATS_STACK = LDS_GND_OFFSET + 2 * NG * LDS_GND_FLOATS;
 static_assert(LDS_FLOATS_STACK * 4 * 64 * 4 <= 160 * 1024, "four Stack workgroups per CU");
 constexpr int PAIR_FLOATS = 21;
 constexpr int GSTASH_PAIR_OFFSET = LDS_STASH_FLOATS + 13;
-// Stack: M^-1 J^T of the normal rows of gripper slots 0 .. GRIP_MJ_SLOTS-1,
-// env-major after the pair rows (9 floats per slot), computed with J at
-// contact setup and loaded at the top of each sweep (object_normals), so a
-// gripper normal updates dv with 9 FMAs instead of the 81 of M^-1 (J^T dl):
-// 7.89 -> 7.60 ms per step at 65 536 envs.  The friction rows' 18 floats per
-// slot the same way (GRIP_MJC_SLOTS) spilled 40-81 VGPRs and ran slower
-// (8.12 ms for 2 slots, 8.76 for 4: profiles/r03j_variants_stack_grip_mj.log).
-#ifndef PS_STACK_GRIP_MJ
-#define PS_STACK_GRIP_MJ NR
-#endif
-constexpr int GRIP_MJ_SLOTS = PS_STACK_GRIP_MJ;
-#ifndef PS_STACK_GRIP_MJC
-#define PS_STACK_GRIP_MJC 0
-#endif
-// and of the friction rows of slots 0 .. GRIP_MJC_SLOTS-1 (18 floats per slot)
-constexpr int GRIP_MJC_SLOTS = PS_STACK_GRIP_MJC;
+// Stack: M^-1 J^T of the gripper slots' normal rows, env-major after the
+// pair rows (9 floats per slot), computed with J at contact setup and loaded
+// at the top of each sweep (object_normals), so a gripper normal updates dv
+// with 9 FMAs instead of the 81 of M^-1 (J^T dl): 7.89 -> 7.60 ms per step at
+// 65 536 envs.  The friction rows' 18 floats per slot the same way spilled
+// 40-81 VGPRs and ran slower (8.12 ms for 2 slots, 8.76 for 4:
+// profiles/r03j_variants_stack_grip_mj.log), so those keep the M^-1 product.
+constexpr int GRIP_MJ_SLOTS = NR;
 constexpr int GSTASH_GRIP_OFFSET = GSTASH_PAIR_OFFSET + NP * PAIR_FLOATS;
-constexpr int GRIP_FLOATS = GRIP_MJ_SLOTS * 9 + GRIP_MJC_SLOTS * 18;
+constexpr int GRIP_FLOATS = GRIP_MJ_SLOTS * 9;
 constexpr int GSTASH_FLOATS = GSTASH_GRIP_OFFSET + GRIP_FLOATS;
 template <int NOBJ>
 constexpr int lds_floats() { return NOBJ == 2 ? LDS_FLOATS_STACK : LDS_FLOATS; }
@@ -648,10 +640,6 @@ struct MJStore {
     // Stack only (global stash): M^-1 J^T of gripper slot c's normal row, element k
     __attribute__((address_space(1))) float *ggrip = nullptr;
     PS_D float &grip(int c, int k) const { return *(float *)&ggrip[c * 9 + k]; }
-    // friction rows 1, 2 of slot c: element k of row j at [GRIP_MJ_SLOTS * 9 + c * 18 + (j - 1) * 9 + k]
-    PS_D float &gripc(int c, int j, int k) const {
-        return *(float *)&ggrip[GRIP_MJ_SLOTS * 9 + c * 18 + (j - 1) * 9 + k];
-    }
     // a copy whose address the compiler cannot see through: loads from it are
     // not loop-invariant, so they stay in the PGS loop as ds_reads instead of
     // being hoisted into (spilled) registers
@@ -660,7 +648,7 @@ struct MJStore {
         asm volatile("" : "+v"(r.base));
         asm volatile("" : "+v"(r.goff));
         asm volatile("" : "+v"(r.gpair));
-        if constexpr (GRIP_MJ_SLOTS + GRIP_MJC_SLOTS > 0) asm volatile("" : "+v"(r.ggrip));
+        asm volatile("" : "+v"(r.ggrip));
         return r;
     }
 };
@@ -1489,10 +1477,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
 #pragma unroll
                         for (int b = 0; b < 9; b++) s += Mi[sidx(a, b)] * c.J[j][b];
                         lds.at(sl, j, a) = NOBJ == 2 ? c.J[j][a] : s;  // Stack: J (M^-1 J^T rebuilt in the loop)
-                        if constexpr (NOBJ == 2 && GRIP_MJ_SLOTS > 0)
-                            if (j == 0 && sl < GRIP_MJ_SLOTS) lds.grip(sl, a) = s;
-                        if constexpr (NOBJ == 2 && GRIP_MJC_SLOTS > 0)
-                            if (j > 0 && sl < GRIP_MJC_SLOTS) lds.gripc(sl, j, a) = s;
+                        if constexpr (NOBJ == 2)
+                            if (j == 0) lds.grip(sl, a) = s;
                         den += c.J[j][a] * s;
                     }
                     float rel = jrow_dot(c.J[j], v1);
@@ -1522,10 +1508,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     for (int a = 0; a < 9; a++) {
                         c.J[j][a] = 0.0f;
                         lds.at(sl, j, a) = 0.0f;
-                        if constexpr (NOBJ == 2 && GRIP_MJ_SLOTS > 0)
-                            if (j == 0 && sl < GRIP_MJ_SLOTS) lds.grip(sl, a) = 0.0f;
-                        if constexpr (NOBJ == 2 && GRIP_MJC_SLOTS > 0)
-                            if (j > 0 && sl < GRIP_MJC_SLOTS) lds.gripc(sl, j, a) = 0.0f;
+                        if constexpr (NOBJ == 2)
+                            if (j == 0) lds.grip(sl, a) = 0.0f;
                     }
                     c.dir[j] = c.rn[j] = mk(0, 0, 0);
                     c.rhs[j] = c.lam[j] = c.dinv[j] = 0.0f;
@@ -1663,9 +1647,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     (void)pair_rel;
     (void)pair_apply;
 
-    // Stack keeps the gripper rows' J, not M^-1 J^T, in LDS: dv += M^-1 g for
-    // the generalized impulse g (J^T dl, or both friction rows' J^T dl summed:
-    // one product with the M^-1 registers per contact and sweep)
+    // Stack keeps the gripper rows' J, not M^-1 J^T, in LDS: the warm start and
+    // the friction rows apply dv += M^-1 g for the generalized impulse g (J^T
+    // dl, or both friction rows' J^T dl summed: one product with the M^-1
+    // registers per contact and sweep); the normal rows read their M^-1 J^T
+    // from the global stash (GRIP_MJ_SLOTS)
     auto mi_apply = [&](const float g[9]) {
 #pragma unroll
         for (int a = 0; a < 9; a++) {
@@ -1733,7 +1719,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             }
     }
 
-    float gmj[GRIP_MJ_SLOTS > 0 ? GRIP_MJ_SLOTS : 1][9];  // Stack: see object_normals
+    float gmj[GRIP_MJ_SLOTS][9];  // Stack: see object_normals
     auto object_normals = [&]() {
         if constexpr (NOBJ == 2) {
         // Stack: the cubes' ground normals and the pair normals touch only
@@ -1760,9 +1746,9 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
-            if constexpr (GRIP_MJ_SLOTS > 0) {
-                // the normal rows' M^-1 J^T of gripper slots 0 .. GRIP_MJ_SLOTS-1,
-                // loaded here so the L2 latency runs under the ground rows
+            {
+                // the gripper normal rows' M^-1 J^T, loaded here so the L2
+                // latency runs under the ground rows
 #pragma unroll
                 for (int c = 0; c < GRIP_MJ_SLOTS; c++)
                     if (gate_robot & (1u << c)) {
@@ -1852,15 +1838,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 dl = nl - r.lam[0];
                 r.lam[0] = nl;
                 if constexpr (NOBJ == 2) {
-                    if (c < GRIP_MJ_SLOTS) {
 #pragma unroll
-                        for (int a = 0; a < 9; a++) dv[a] = fmaf(gmj[c < GRIP_MJ_SLOTS ? c : 0][a], dl, dv[a]);
-                    } else {
-                        float g[9];
-#pragma unroll
-                        for (int a = 0; a < 9; a++) g[a] = Jl[a] * dl;
-                        mi_apply(g);
-                    }
+                    for (int a = 0; a < 9; a++) dv[a] = fmaf(gmj[c][a], dl, dv[a]);
                 } else {
 #pragma unroll
                     for (int a = 0; a < 9; a++) dv[a] = fmaf(mj[a], dl, dv[a]);
@@ -1892,21 +1871,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        float gmc[GRIP_MJC_SLOTS > 0 ? GRIP_MJC_SLOTS : 1][18];
-        if constexpr (NOBJ == 2 && GRIP_MJC_SLOTS > 0) {
-            // the friction rows' M^-1 J^T of gripper slots 0 .. GRIP_MJC_SLOTS-1,
-            // loaded ahead of the ground cones
-#pragma unroll
-            for (int c = 0; c < GRIP_MJC_SLOTS; c++)
-                if (gate_robot & (1u << c)) {
-#pragma unroll
-                    for (int k = 0; k < 9; k++) {
-                        gmc[c][k] = L.gripc(c, 1, k);
-                        gmc[c][9 + k] = L.gripc(c, 2, k);
-                    }
-                }
-            __builtin_amdgcn_sched_barrier(0);
-        }
+
 #pragma unroll
         for (int b = 0; b < NOBJ; b++) {
             const float inv_m = od[b].inv_m;
@@ -2020,16 +1985,10 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 r.lam[1] = sa;
                 r.lam[2] = sb;
                 if constexpr (NOBJ == 2) {
-                    if (c < GRIP_MJC_SLOTS) {
-                        const int cc = c < GRIP_MJC_SLOTS ? c : 0;
+                    float g[9];
 #pragma unroll
-                        for (int a = 0; a < 9; a++) dv[a] = fmaf(gmc[cc][9 + a], dlb, fmaf(gmc[cc][a], dla, dv[a]));
-                    } else {
-                        float g[9];
-#pragma unroll
-                        for (int a = 0; a < 9; a++) g[a] = fmaf(J2[a], dlb, J1[a] * dla);
-                        mi_apply(g);
-                    }
+                    for (int a = 0; a < 9; a++) g[a] = fmaf(J2[a], dlb, J1[a] * dla);
+                    mi_apply(g);
                 } else {
 #pragma unroll
                     for (int a = 0; a < 9; a++) dv[a] = fmaf(mj2[a], dlb, fmaf(mj1[a], dla, dv[a]));

@@ -19,12 +19,6 @@ VARIANTS = {
     # IEEE mode off: drops the v_max x,x,x canonicalisations before min/max
     # (68 of ~3000 instructions in the Push PGS loop); NaN handling only
     "ieee_off": ["-fno-honor-nans", "-mno-amdgpu-ieee"],
-    # Stack: M^-1 J^T of gripper slots 0..n-1 from the global stash, normal rows
-    # (PS_STACK_GRIP_MJ, the product uses 4) and friction rows (PS_STACK_GRIP_MJC)
-    "smj0": ["-DPS_STACK_GRIP_MJ=0"],
-    "smj2": ["-DPS_STACK_GRIP_MJ=2"],
-    "smj4c2": ["-DPS_STACK_GRIP_MJC=2"],
-    "smj4c4": ["-DPS_STACK_GRIP_MJC=4"],
     # group-kernel miscompute bisection
     "o1": ["-O1"],
     "prealloc": ["-mllvm", "-amdgpu-prealloc-sgpr-spill-vgprs=1"],
