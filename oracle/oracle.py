@@ -119,6 +119,8 @@ def lib():
         L.po_set_link_aabb.argtypes = [I, D, D, D]
         L.po_set_finger_noise.argtypes = [D, C.c_uint64]
         L.po_set_state_noise.argtypes = [D, C.c_uint64]
+        L.po_set_pgs_log.argtypes = [C.c_void_p, C.c_int64]
+        L.po_set_pgs_log.restype = C.c_int64
         _lib = L
     return _lib
 

@@ -1087,6 +1087,19 @@ static void ulp_noise(double *x, int n) {
     }
 }
 
+/* Test hook (never part of the restated algorithm): each substep appends its
+ * PGS iteration count to a caller buffer while one is set (serial use only;
+ * scripts/pgs_iteration_stats.py). */
+static int32_t *pgs_log = NULL;
+static int64_t pgs_log_cap = 0, pgs_log_n = 0;
+int64_t po_set_pgs_log(int32_t *buf, int64_t cap) {
+    const int64_t n = pgs_log_n;
+    pgs_log = buf;
+    pgs_log_cap = buf ? cap : 0;
+    pgs_log_n = 0;
+    return n;
+}
+
 /* Event signatures of a substep (test bookkeeping): the ordered contact
  * features (cache group and id; object-object contacts by count) with the
  * arm's joint-limit rows (joint and side), and separately the finger joints'
@@ -1289,6 +1302,7 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
         if (res <= PM_SOLVER_RESIDUAL_THRESHOLD || it >= PM_SOLVER_ITERATIONS - 1) break;
     }
     cache_store(&env->cache, cts, nc, rows + normal_base);
+    if (pgs_log && pgs_log_n < pgs_log_cap) pgs_log[pgs_log_n++] = it + 1;
     if (stats) {
         int64_t n_it = it + 1, n_lim = 0, n_mot = n_noncontact, nk[4] = {0, 0, 0, 0};
         for (int j = 0; j < n_noncontact; j++) n_lim += rows[j].hi == PM_LIMIT_MAX_IMPULSE && rows[j].lo == 0.0;

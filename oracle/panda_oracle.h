@@ -160,6 +160,9 @@ void po_set_finger_noise(double amplitude, uint64_t seed);
  * and velocities) moves by u * ulp32(x), u uniform in [-ulps, ulps] -- the
  * fp32 resolution of the state (0 = off), not thread-safe */
 void po_set_state_noise(double ulps, uint64_t seed);
+/* test hook: while buf != NULL every substep appends its PGS iteration count
+ * (up to cap entries); returns the entries the previous buffer received */
+int64_t po_set_pgs_log(int32_t *buf, int64_t cap);
 
 #ifdef __cplusplus
 }

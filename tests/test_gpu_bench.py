@@ -69,3 +69,45 @@ def test_bench_single_rank_roofline_blocks():
     assert set(fp["split"]) == {"dynamics_and_rows", "pgs", "ik", "step"}
     cb = line["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
+
+
+_RCCL_ONE_RANK = r"""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, os.path.join(os.environ["ROOT"], "panda-lang-manip_amd"))
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+assert dist.get_backend() == "nccl"
+import pandasim
+from pandasim.dist import EpisodeStats, gather_to_rank0, max_over_ranks
+B = 300
+env = pandasim.make("PandaPush-v3", num_envs=B, device=dev)
+env.reset(seed=5)
+stats = EpisodeStats(B, dev)
+g = torch.Generator(device=dev)
+g.manual_seed(3)
+for _ in range(55):
+    _, r, te, tr, _ = env.step(torch.rand(B, 3, device=dev, generator=g) * 2 - 1, copy=False)
+    stats.update(r, te, tr)
+local = stats.packed()
+full = gather_to_rank0(local)
+assert full is not None and torch.equal(full, local), "RCCL gather changed the statistics"
+assert int(local[2].sum()) >= B  # every env finished an episode (TimeLimit 50)
+assert max_over_ranks(1.25, dev) == 1.25
+dist.barrier()
+dist.destroy_process_group()
+print("RCCL_OK")
+"""
+
+
+def test_rccl_one_rank_gather_and_max():
+    """The bench's collectives (pandasim.dist: the all_gather of shard sizes,
+    the gather of episode statistics to rank 0, the max-over-ranks timer)
+    through a real RCCL ("nccl") process group.  One box has one GPU and RCCL
+    takes one rank per GPU, so this is world size 1; the 2-rank path is
+    rehearsed under gloo above and the 8-GPU run is the driver's."""
+    env = dict(os.environ, ROOT=ROOT, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+               HSA_ENABLE_IPC_MODE_LEGACY="0")
+    out = subprocess.run([sys.executable, "-c", _RCCL_ONE_RANK], capture_output=True, text=True, timeout=240,
+                         env=env, cwd=ROOT)
+    assert out.returncode == 0 and "RCCL_OK" in out.stdout, (out.stdout[-1500:], out.stderr[-3000:])
