@@ -2120,6 +2120,13 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         pt.acc[9] += wmax;
         pt.acc[10] += 1;
         pt.acc[11] += wnr;
+        // the wave's open row gates (wave-uniform: every lane adds the same)
+        unsigned ngnd = 0;
+        for (int b = 0; b < NB; b++) ngnd += __builtin_popcount(gate_ground[b]);
+        pt.acc[12] += __builtin_popcount(gate_pair);
+        pt.acc[13] += ngnd;
+        pt.acc[14] += __builtin_popcount(gate_robot);
+        pt.acc[15] += gate_lim != 0u;
     }
 #endif
     {

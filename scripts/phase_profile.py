@@ -28,7 +28,7 @@ def main():
     env.reset(seed=12345)
     lib = L.lib()
     lib.ps_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int]
-    buf = (C.c_ulonglong * 12)()
+    buf = (C.c_ulonglong * 16)()
     g = torch.Generator(device="cuda")
     g.manual_seed(0xC0FFEE)
     for k in range(5):
@@ -47,6 +47,8 @@ def main():
     subs = buf[10]  # wave-substeps counted by lane 0 of each wave
     print(f"  PGS iterations per substep: lane-0 mean {buf[8] / subs:.2f}, wave max {buf[9] / subs:.2f}; "
           f"max robot contacts per wave {buf[11] / subs:.2f}")
+    print(f"  open row gates per wave-substep: pair slots {buf[12] / subs:.2f}, ground slots {buf[13] / subs:.2f}, "
+          f"robot slots {buf[14] / subs:.2f}, joint limits {buf[15] / subs:.2f}")
 
 
 if __name__ == "__main__":

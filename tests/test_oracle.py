@@ -463,3 +463,78 @@ def test_coriolis_terms_follow_from_the_mass_matrix():
                        for e in np.eye(9)])  # dM[k] = dM/dq_k
         cqd = np.einsum("kij,j,k->i", dM, qd, qd) - 0.5 * np.einsum("ijk,j,k->i", dM, qd, qd)
         assert np.allclose(even, cqd, rtol=1e-5, atol=1e-7), (even, cqd)
+
+
+# ---- contact mechanics identities (independent of PyBullet: Coulomb friction
+# and statics).  The contact constants the oracle shares with the kernels
+# (include/panda_model.h) cannot show up in GPU-vs-oracle tests; these pin the
+# oracle's contact solve to mechanics itself.
+
+def _sliding_run(task, v0, steps=80, settle=25):
+    """The task's object alone on its table (no robot), settled, then given a
+    horizontal velocity v0 (m/s, 2-vector); returns (cfg, mu, p0, positions,
+    velocities, angular velocities) per step."""
+    cfg = O.config(task, has_robot=0, has_plane=0)
+    env = O.new_env(cfg)
+    O.reset(cfg, env, seed=1)
+    for _ in range(settle):
+        O.sim_step(cfg, env)
+    p0 = np.array(env.obj[0].pos)
+    env.obj[0].vel[0], env.obj[0].vel[1] = v0
+    ps, vs, ws = [], [], []
+    for _ in range(steps):
+        O.sim_step(cfg, env)
+        ps.append(np.array(env.obj[0].pos))
+        vs.append(np.array(env.obj[0].vel))
+        ws.append(np.array(env.obj[0].omg))
+    # friction coefficients multiply (object x table 0.5; panda_oracle.c contact setup)
+    mu = cfg.object_friction * 0.5
+    return cfg, mu, p0, np.array(ps), np.array(vs), np.array(ws)
+
+
+@pytest.mark.parametrize("task,v0,tol", [("push", (-0.5, 0.0), 0.02), ("push", (-0.6, 0.45), 0.02),
+                                         ("pick_and_place", (-1.0, 0.0), 0.02), ("slide", (-0.3, 0.1), 0.06)])
+def test_sliding_object_decelerates_at_mu_g(task, v0, tol):
+    """A cube (cylinder for Slide) sliding on the table: Coulomb friction
+    decelerates it at mu g along its velocity, it stops after v0^2 / (2 mu g),
+    and it neither lifts, sinks nor turns (the four corner contacts share the
+    load).  tol: relative (the cylinder's ground contacts tilt its friction
+    cone's support by a few percent)."""
+    cfg, mu, p0, ps, vs, ws = _sliding_run(task, v0)
+    g = 9.81
+    speed0 = float(np.hypot(*v0))
+    speed = np.hypot(vs[:, 0], vs[:, 1])
+    t = 0.04 * (np.arange(len(speed)) + 1)
+    moving = speed > 0.05
+    decel = -np.polyfit(t[moving], speed[moving], 1)[0]
+    assert abs(decel - mu * g) <= tol * mu * g, (decel, mu * g)
+    dist = float(np.hypot(*(ps[-1, :2] - p0[:2])))
+    assert abs(dist - speed0 ** 2 / (2 * mu * g)) <= 2.5 * tol * speed0 ** 2 / (2 * mu * g), dist
+    assert speed[-1] < 1e-3  # at rest again
+    # the path is straight along v0
+    d = (ps[-1, :2] - p0[:2]) / dist
+    assert abs(d @ np.array(v0) / speed0 - 1.0) < 1e-3
+    assert np.all(np.abs(ps[:, 2] - p0[2]) < 2e-4) and np.all(np.abs(ws) < 0.05)
+
+
+@pytest.mark.parametrize("task", ["push", "slide", "pick_and_place"])
+def test_resting_object_normal_impulses_carry_its_weight(task):
+    """Statics of the warm-started solve: a settled object's ground normal
+    impulses (the contact cache the next substep starts from) sum to m g dt
+    per substep, and it does not drift faster than the solver resolves: PGS
+    stops at a squared row residual of 1e-7, so a tangential creep below
+    sqrt(1e-7) = 3.2e-4 m/s is left alone by the friction rows (a cube settles
+    with ~3e-5 m/s of creep, as Bullet's early-terminated solve allows)."""
+    cfg = O.config(task, has_robot=0, has_plane=0)
+    env = O.new_env(cfg)
+    O.reset(cfg, env, seed=3)
+    for _ in range(25):
+        O.sim_step(cfg, env)
+    p = np.array(env.obj[0].pos)
+    for _ in range(25):
+        O.sim_step(cfg, env)
+    lam = sum(env.cache.ground_lam[0][k] for k in range(4))
+    assert abs(lam - cfg.object_mass * 9.81 / 500) < 1e-9 * cfg.object_mass
+    assert np.all(np.abs(np.array(env.obj[0].pos) - p) < 1e-4)
+    assert abs(env.obj[0].pos[2] - p[2]) < 1e-8
+    assert np.all(np.abs(np.array(env.obj[0].vel)) < 1e-4)
