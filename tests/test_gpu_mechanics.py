@@ -22,17 +22,18 @@ def _scene(env_id, B, seed):
     return env, env.sim
 
 
-def _velocities(B, rng):
-    """Speeds 0.2-0.6 m/s pointing into the table (-x half-plane, so the
+def _velocities(B, rng, lo=0.5, hi=1.0):
+    """Speeds lo-hi m/s pointing into the table (the -x half-plane, so the
     object stops before an edge)."""
-    speed = rng.uniform(0.2, 0.6, B)
+    speed = rng.uniform(lo, hi, B)
     ang = rng.uniform(np.pi * 0.75, np.pi * 1.25, B)
     return np.stack([speed * np.cos(ang), speed * np.sin(ang)], axis=1)
 
 
-@pytest.mark.parametrize("env_id,mu,tol", [("PandaPush-v3", 0.25, 0.02), ("PandaPickAndPlace-v3", 0.25, 0.02),
-                                           ("PandaSlide-v3", 0.02, 0.06)])
-def test_gpu_sliding_object_decelerates_at_mu_g(env_id, mu, tol):
+@pytest.mark.parametrize("env_id,mu,tol,speeds", [("PandaPush-v3", 0.25, 0.02, (0.5, 1.0)),
+                                                  ("PandaPickAndPlace-v3", 0.25, 0.02, (0.5, 1.0)),
+                                                  ("PandaSlide-v3", 0.02, 0.06, (0.15, 0.3))])
+def test_gpu_sliding_object_decelerates_at_mu_g(env_id, mu, tol, speeds):
     from pandasim import _lib as L
 
     B, T = 64, 60
@@ -40,7 +41,7 @@ def test_gpu_sliding_object_decelerates_at_mu_g(env_id, mu, tol):
     for _ in range(25):
         sim.step()
     p0 = sim.rows(L.F_CPOS, 3).clone()
-    v0 = _velocities(B, np.random.default_rng(5))
+    v0 = _velocities(B, np.random.default_rng(5), *speeds)
     vel = sim.rows(L.F_CVEL, 3).clone()
     vel[:, :2] = torch.as_tensor(v0, dtype=torch.float32, device=vel.device)
     sim.set_rows(L.F_CVEL, vel)
@@ -56,7 +57,8 @@ def test_gpu_sliding_object_decelerates_at_mu_g(env_id, mu, tol):
     for i in range(B):
         speed0 = float(np.hypot(*v0[i]))
         speed = np.hypot(vs[:, i, 0], vs[:, i, 1])
-        moving = speed > 0.05
+        moving = speed > 0.1 * speed0
+        assert moving.sum() >= 4, i
         decel = -np.polyfit(t[moving], speed[moving], 1)[0]
         assert abs(decel - mu * G) <= tol * mu * G, (i, decel, mu * G)
         stop = speed0 ** 2 / (2 * mu * G)

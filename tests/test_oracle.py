@@ -505,7 +505,7 @@ def test_sliding_object_decelerates_at_mu_g(task, v0, tol):
     speed0 = float(np.hypot(*v0))
     speed = np.hypot(vs[:, 0], vs[:, 1])
     t = 0.04 * (np.arange(len(speed)) + 1)
-    moving = speed > 0.05
+    moving = speed > 0.1 * speed0
     decel = -np.polyfit(t[moving], speed[moving], 1)[0]
     assert abs(decel - mu * g) <= tol * mu * g, (decel, mu * g)
     dist = float(np.hypot(*(ps[-1, :2] - p0[:2])))
