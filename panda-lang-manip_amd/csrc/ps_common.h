@@ -19,8 +19,10 @@
 // each wave accumulates s_memtime deltas per phase and lane 0 adds them to
 // ps_phase_cycles at the end of the kernel.  Compiled out of the product.
 #define PS_NUM_PHASES 8
-#define PS_NUM_PROF_SLOTS 16  // phases + PGS counters (lane iterations, wave iterations, substeps, robot-contact slots run,
-                              // and the wave's open row gates: pair slots, ground slots, robot slots, joint limits)
+#define PS_NUM_PROF_SLOTS 20  // phases + PGS counters (lane iterations, wave iterations, substeps, robot-contact slots run,
+                              // the wave's open row gates: pair slots, ground slots, robot slots, joint limits;
+                              // 16-18: sub-phases of rows+contacts -- joint rows, object ground/pair contacts,
+                              // gripper contact candidates -- the rest of it, the gripper rows, stays in 3)
 #ifdef PS_PROFILE_PHASES
 struct PhaseTimer {
     uint64_t last, acc[PS_NUM_PROF_SLOTS];

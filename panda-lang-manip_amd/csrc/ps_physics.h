@@ -1228,6 +1228,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         mot_lam[d] = 0.0f;
     }
 
+    PS_PHASE(16);
     // ---- contacts (oracle gen_contacts order: ground per object, pairs, gripper)
     GroundContact gc[NB][NG];
     int ng[NB];
@@ -1392,6 +1393,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     RobotContact rc[NR];
     int nr = 0;
     {
+        PS_PHASE(17);
         // 1) candidate gripper contacts in spec order (spheres vs object 1,
         //    vs object 2, then spheres vs ground) -> small records; the first
         //    NR active ones are assigned slots 0..NR-1 (select into
@@ -1439,6 +1441,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 }
             }
         });
+        PS_PHASE(18);
         // 2) rows of each used slot: J (registers), M^-1 J^T (LDS), rhs, bounds;
         //    the normal starts from the cached impulse of the same feature
         float prl[NR];

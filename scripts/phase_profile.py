@@ -28,7 +28,7 @@ def main():
     env.reset(seed=12345)
     lib = L.lib()
     lib.ps_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int]
-    buf = (C.c_ulonglong * 16)()
+    buf = (C.c_ulonglong * 20)()
     g = torch.Generator(device="cuda")
     g.manual_seed(0xC0FFEE)
     for k in range(5):
@@ -39,11 +39,17 @@ def main():
         env.step(torch.rand(B, env.action_dim, device="cuda", generator=g) * 2 - 1, copy=False)
     torch.cuda.synchronize()
     assert lib.ps_debug_phase_cycles(buf, 0) == 0
+    # rows+contacts (slot 3) keeps the gripper rows; slots 16-18 hold its other parts
+    buf[3] += buf[16] + buf[17] + buf[18]
     tot = sum(buf[:8])
     waves = (B * env.lanes_per_env + 63) // 64
     print(f"{env_id} B={B} lanes/env={env.lanes_per_env}: {tot / waves / steps:.0f} wave-cycles per wave-step")
     for n, v in zip(NAMES, buf[:8]):
         print(f"  {n:24s} {v / tot * 100:6.2f} %   {v / waves / steps / 20:10.0f} cyc/substep-equiv")
+    if buf[3]:
+        parts = (("joint rows", buf[16]), ("object contacts", buf[17]), ("gripper candidates", buf[18]),
+                 ("gripper rows", buf[3] - buf[16] - buf[17] - buf[18]))
+        print("  rows+contacts split: " + ", ".join(f"{n} {v / buf[3] * 100:.1f} %" for n, v in parts))
     subs = buf[10]  # wave-substeps counted by lane 0 of each wave
     print(f"  PGS iterations per substep: lane-0 mean {buf[8] / subs:.2f}, wave max {buf[9] / subs:.2f}; "
           f"max robot contacts per wave {buf[11] / subs:.2f}")

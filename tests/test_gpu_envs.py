@@ -121,3 +121,38 @@ def test_motor_gain_rows_follow_the_fused_step():
     env.step(a)
     kp_kd_vel2, imp2 = gains()
     assert torch.equal(kp_kd_vel2, kp_kd_vel) and torch.equal(imp2, imp)
+
+
+@pytest.mark.parametrize("cls_name,env_id", [("PandaPushGymEnv", "PandaPush-v3"),
+                                             ("PandaStackGymEnv", "PandaStackJointsDense-v3")])
+def test_one_env_gymnasium_api(cls_name, env_id):
+    """The gym.make entry points (pandasim.gym_registration): numpy obs dicts,
+    float rewards, bool flags, the TimeLimit truncation, and the same bits as
+    a one-env PandaVecEnv without auto-reset."""
+    import pandasim
+    from pandasim import gym_registration as GR
+    from pandasim.envs import REGISTRY
+
+    spec = REGISTRY[env_id]
+    env = getattr(GR, cls_name)(reward_type=spec["reward_type"], control_type=spec["control_type"])
+    ref = pandasim.make(env_id, num_envs=1, autoreset=False)
+    obs, info = env.reset(seed=3)
+    robs, _ = ref.reset(seed=3)
+    assert set(obs) == {"observation", "achieved_goal", "desired_goal"} and isinstance(info["is_success"], bool)
+    for k in obs:
+        assert obs[k].dtype == np.float32 and np.array_equal(obs[k], robs[k][0].cpu().numpy())
+    rng = np.random.default_rng(0)
+    steps = spec["max_episode_steps"]
+    for t in range(steps):
+        a = rng.uniform(-1, 1, env._env.action_dim).astype(np.float32)
+        obs, r, te, tr, info = env.step(a)
+        robs, rr, rte, rtr, _ = ref.step(torch.as_tensor(a, device="cuda").reshape(1, -1))
+        assert isinstance(r, float) and isinstance(te, bool) and isinstance(tr, bool)
+        assert r == float(rr[0]) and te == bool(rte[0]) and tr == bool(rtr[0])
+        for k in obs:
+            assert np.array_equal(obs[k], robs[k][0].cpu().numpy()), (t, k)
+        assert tr == (t == steps - 1)
+    her = env.compute_reward(obs["achieved_goal"][None], obs["desired_goal"][None])
+    # HER recomputes from the float32 goals of the observation; the step used
+    # the float64 desired goal (as numpy does in the reference): rounding apart
+    assert her.shape == (1,) and abs(float(her[0]) - r) <= 1e-6

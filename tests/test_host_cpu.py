@@ -180,3 +180,59 @@ def test_finger_pad_proxies_sit_on_the_pads():
         y_open = abs(cy) + q_open  # finger frame y plus the prismatic opening, hand frame
         assert abs(y_open - pad_y_open) <= r, (link, y_open)
         assert mu == 1.0  # panda.py:47-48
+
+
+def test_gymnasium_registration_mirrors_the_reference(monkeypatch):
+    """register_envs() registers the reference's 24 IDs
+    (panda_gym/__init__.py:8-54: 6 tasks x {sparse, dense} x {ee, joints},
+    kwargs reward_type/control_type, max_episode_steps 50, Stack 100) with
+    gymnasium -- checked against a stand-in registry, as gymnasium is not
+    installed in this image."""
+    import importlib
+    import sys
+    import types
+
+    calls = []
+    gym = types.ModuleType("gymnasium")
+    gym.Env = type("Env", (), {})
+    envs_mod = types.ModuleType("gymnasium.envs")
+    reg_mod = types.ModuleType("gymnasium.envs.registration")
+    reg_mod.registry = {}
+
+    def register(id, entry_point, kwargs, max_episode_steps):
+        calls.append((id, entry_point, kwargs, max_episode_steps))
+        reg_mod.registry[id] = entry_point
+
+    reg_mod.register = register
+    gym.envs = envs_mod
+    envs_mod.registration = reg_mod
+    for name, mod in (("gymnasium", gym), ("gymnasium.envs", envs_mod), ("gymnasium.envs.registration", reg_mod)):
+        monkeypatch.setitem(sys.modules, name, mod)
+    import pandasim.gym_registration as GR
+
+    GR = importlib.reload(GR)
+    try:
+        ids = GR.register_envs()
+        expected = []
+        for reward_type in ("sparse", "dense"):
+            for control_type in ("ee", "joints"):
+                for name, steps in (("Reach", 50), ("Push", 50), ("Slide", 50), ("PickAndPlace", 50), ("Stack", 100),
+                                    ("Flip", 50)):
+                    expected.append(("Panda{}{}{}-v3".format(name, "Joints" if control_type == "joints" else "",
+                                                             "Dense" if reward_type == "dense" else ""),
+                                     {"reward_type": reward_type, "control_type": control_type}, steps, name))
+        assert ids == [e[0] for e in expected] and len(set(ids)) == 24
+        for (cid, entry, kwargs, steps), (eid, ekw, esteps, name) in zip(calls, expected):
+            assert (cid, kwargs, steps) == (eid, ekw, esteps)
+            mod, cls = entry.split(":")
+            assert mod == "pandasim.gym_registration" and cls == f"Panda{name}GymEnv"
+            assert issubclass(getattr(GR, cls), gym.Env)
+        # idempotent: a second call registers nothing new
+        n = len(calls)
+        GR.register_envs()
+        assert len(calls) == n
+    finally:
+        monkeypatch.undo()
+        importlib.reload(GR)
+    with pytest.raises(ImportError):
+        GR.register_envs()
