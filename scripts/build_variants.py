@@ -19,6 +19,10 @@ VARIANTS = {
     # IEEE mode off: drops the v_max x,x,x canonicalisations before min/max
     # (68 of ~3000 instructions in the Push PGS loop); NaN handling only
     "ieee_off": ["-fno-honor-nans", "-mno-amdgpu-ieee"],
+    "trackers": ["-mllvm", "-amdgpu-use-amdgpu-trackers"],
+    "no_unclust": ["-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule"],
+    "trk_nu": ["-mllvm", "-amdgpu-use-amdgpu-trackers", "-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule"],
+    "trk_ilpmin": ["-mllvm", "-amdgpu-use-amdgpu-trackers", "-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
     # group-kernel miscompute bisection
     "o1": ["-O1"],
     "prealloc": ["-mllvm", "-amdgpu-prealloc-sgpr-spill-vgprs=1"],
@@ -27,7 +31,25 @@ VARIANTS = {
 
 
 # variants that change the per-unit flags of build.UNITS instead
+_TRK = ["-mllvm", "-amdgpu-use-amdgpu-trackers"]
+_CLAUSE = ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]
+
+
+def _one_lane(units, flags_of_task):
+    out = []
+    for n, s, defs in units:
+        if n.startswith("step_t") and not n.endswith("_groups"):
+            defs = [d for d in defs if d not in _TRK + _CLAUSE] + flags_of_task(int(n[6]))
+        out.append((n, s, defs))
+    return out
+
+
 UNIT_VARIANTS = {
+    # scheduler options on the one-lane step objects only
+    "onelane_trk": lambda units: _one_lane(units, lambda t: _TRK),
+    "onelane_trk_clause": lambda units: _one_lane(units, lambda t: _TRK + (_CLAUSE if t != 4 else [])),
+    # the product before r03k: no scheduler options on the one-lane objects
+    "onelane_plain": lambda units: [(n, s, [d for d in defs if d not in _TRK + _CLAUSE]) for n, s, defs in units],
     # the group-kernel objects at the library's -O3 (the product builds them at
     # -O1)
     "groups_o3": lambda units: [(n, s, [d for d in defs if d != "-O1"]) for n, s, defs in units],
