@@ -281,7 +281,7 @@ def main():
             raise SystemExit(f"bench.py: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
 
     import pandasim
-    from pandasim.dist import EpisodeStats, gather_to_rank0, max_over_ranks, shard_seeds
+    from pandasim.dist import gather_to_rank0, max_over_ranks, shard_seeds
     from pandasim.envs import REGISTRY
 
     B = args.batch
@@ -293,13 +293,15 @@ def main():
     gen.manual_seed(0xC0FFEE + rank)
     n_act = args.warmup + args.steps
     actions = torch.rand(n_act, B, env.action_dim, device=dev, generator=gen) * 2 - 1
-    stats = EpisodeStats(B, dev)
+    # episode returns and successes, accumulated inside the step kernel
+    # (RecordEpisodeStatistics fused: ps_set_episode_stats); rows 1-3 are
+    # EpisodeStats.packed()'s layout
+    eps = env.record_episode_statistics()
 
     for k in range(args.warmup):
         obs, r, te, tr, info = env.step(actions[k], copy=False)
-        stats.update(r, te, tr)  # also loads every kernel the timed loop uses
-    gather_to_rank0(stats.packed())
-    stats = EpisodeStats(B, dev)
+    gather_to_rank0(eps[1:].contiguous())  # also loads the collective path
+    eps.zero_()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -312,9 +314,8 @@ def main():
         starts[k].record()
         obs, r, te, tr, info = env.step(a, copy=False)
         stops[k].record()
-        stats.update(r, te, tr)
     # the one collective of the path: episode statistics to rank 0 (RCCL over xGMI)
-    episode_stats = gather_to_rank0(stats.packed())
+    episode_stats = gather_to_rank0(eps[1:].contiguous())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

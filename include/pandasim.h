@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define PS_ABI_VERSION 5
+#define PS_ABI_VERSION 6
 
 /* the six registered tasks (panda_gym/__init__.py:8-54) */
 enum {
@@ -170,6 +170,16 @@ int ps_step(ps_ctx *ctx, void *state, const float *actions, float *obs, float *a
 #define PS_GROUP8_AUTO_MAX_ENVS 8192
 int ps_set_lanes_per_env(ps_ctx *ctx, int lanes);
 int ps_step_lanes(const ps_ctx *ctx); /* the value ps_step uses */
+
+/* gymnasium's RecordEpisodeStatistics, fused into ps_step (no reference
+ * counterpart: the training loop's wrapper around gym.make).  stats != NULL:
+ * device [4, B] f32, caller-owned, must outlive the steps: row 0 the running
+ * return of each env's current episode, row 1 the return of its last finished
+ * episode, row 2 that episode's success (terminated: 1, truncated: 0), row 3
+ * the number of finished episodes.  Every following ps_step adds its reward
+ * to row 0 and, when the episode ends, moves it to row 1 and clears it.
+ * stats == NULL turns it off. */
+int ps_set_episode_stats(ps_ctx *ctx, float *stats);
 
 /* NaN/Inf guard of ps_step (no reference counterpart; SURVEY.md §5 failure
  * detection): with flags != NULL (device [B] u8, caller-owned, must outlive

@@ -748,6 +748,12 @@ int ps_step_lanes(const ps_ctx *c) {
     return c->num_envs <= PS_GROUP8_AUTO_MAX_ENVS ? 8 : 1;
 }
 
+int ps_set_episode_stats(ps_ctx *c, float *stats) {
+    if (!c) return PS_ERR_ARG;
+    c->epstats = stats;
+    return PS_OK;
+}
+
 int ps_set_nonfinite_guard(ps_ctx *c, uint8_t *flags, int reset_nonfinite) {
     if (!c) return PS_ERR_ARG;
     c->nonfinite = flags;

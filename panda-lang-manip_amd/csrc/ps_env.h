@@ -30,6 +30,7 @@ struct ps_ctx {
     int lanes_per_env;    // ps_set_lanes_per_env: 0 auto, 1 or 16
     int gains_dirty;      // the state's motor gain rows may differ from the fused step's (store_motor_gains)
     const void *gains_state;  // the state buffer whose gain rows the last successful ps_step wrote
+    float *epstats;       // ps_set_episode_stats: caller-owned [4][num_envs] f32, or NULL
 };
 
 // arguments of ps_step that the step launchers pass through
@@ -160,6 +161,8 @@ struct KParams {
     int reset_nonfinite;
     float *gstash;  // Stack: GSTASH_FLOATS x stride per-substep stash and pair rows (ctx scratch)
     int write_gains;  // k_step also stores the motor gain rows (ps_ctx::gains_dirty)
+    float *epstats;   // ps_set_episode_stats: [4][epstride] running return, last return, last success, episodes
+    int64_t epstride;
 #ifdef PS_PROFILE_PHASES
     unsigned long long *prof;  // phase counters (ps_prof_buffer)
 #endif
@@ -566,6 +569,8 @@ inline KParams params_of(ps_ctx *c, void *state) {
     P.nonfinite = nullptr;
     P.reset_nonfinite = 0;
     P.write_gains = 0;
+    P.epstats = c->epstats;
+    P.epstride = c->num_envs;
 #ifdef PS_PROFILE_PHASES
     P.prof = ps_prof_buffer();
 #endif
@@ -652,8 +657,9 @@ __global__ __launch_bounds__(kBlock, PS_STEP_MIN_WAVES) void k_step(KParams P, c
     bool term = dist < T::THRESHOLD;
     int el = s.E(i) + 1;
     bool trunc = el >= T::STEPS;
+    const float rew = reward_for(P.reward_type, dist, T::THRESHOLD);
     if (writer) {
-        reward[i] = reward_for(P.reward_type, dist, T::THRESHOLD);
+        reward[i] = rew;
         terminated[i] = term;
         truncated[i] = trunc;
     }
@@ -690,6 +696,22 @@ __global__ __launch_bounds__(kBlock, PS_STEP_MIN_WAVES) void k_step(KParams P, c
         el = 0;
     } else if (writer && (final_obs || final_ag)) {
         write_obs<TASK>(P, i, q, qd, bd, g, final_obs, final_ag, nullptr);
+    }
+    if (writer && P.epstats) {
+        // RecordEpisodeStatistics, fused (ps_set_episode_stats): the running
+        // return of the episode, and at its end (terminated or truncated,
+        // incl. the guard's reset) the finished episode's return and success
+        float *e = P.epstats + i;
+        const int64_t w = P.epstride;
+        const float run = e[0] + rew;
+        if (term || trunc) {
+            e[w] = run;
+            e[2 * w] = term ? 1.0f : 0.0f;
+            e[3 * w] += 1.0f;
+            e[0] = 0.0f;
+        } else {
+            e[0] = run;
+        }
     }
     if (writer) {
         s.E(i) = el;

@@ -69,7 +69,7 @@ def exported_symbols():
         "ps_step", "ps_sim_step", "ps_link_state", "ps_inverse_kinematics", "ps_compute_reward", "ps_rng_seed",
         "ps_rng_uniform", "ps_rng_rotation", "ps_base_state", "ps_camera", "ps_render", "ps_deproject_image",
         "ps_deproject_pixels", "ps_set_nonfinite_guard", "ps_set_lanes_per_env", "ps_step_lanes",
-        "ps_mark_motor_rows_dirty",
+        "ps_mark_motor_rows_dirty", "ps_set_episode_stats",
     ]
 
 
@@ -130,6 +130,7 @@ def lib():
     L.ps_set_lanes_per_env.argtypes = [V, I]
     L.ps_step_lanes.argtypes = [V]
     L.ps_mark_motor_rows_dirty.argtypes = [V]
+    L.ps_set_episode_stats.argtypes = [V, V]
     L.ps_link_state.argtypes = [V, V, I, V, V, V, V, V]
     L.ps_inverse_kinematics.argtypes = [V, V, I, V, V, V, V]
     L.ps_compute_reward.argtypes = [I, I, V, I, V, I, V, V, I64, V]

@@ -68,6 +68,7 @@ class PandaVecEnv:
         self._saved_goals: Dict[int, torch.Tensor] = {}
         self._has_reset = False
         self._nonfinite: Optional[torch.Tensor] = None
+        self._epstats: Optional[torch.Tensor] = None
 
     def set_nonfinite_guard(self, enabled: bool = True, reset: bool = False) -> None:
         """NaN/Inf guard of the fused step (ps_set_nonfinite_guard): step()'s
@@ -78,6 +79,16 @@ class PandaVecEnv:
         else:
             self._nonfinite = None
         self.sim._call("ps_set_nonfinite_guard", self.sim._ctx, _ptr(self._nonfinite), int(bool(enabled and reset)))
+
+    def record_episode_statistics(self, enabled: bool = True) -> Optional[torch.Tensor]:
+        """gymnasium's RecordEpisodeStatistics, fused into the step kernel
+        (ps_set_episode_stats): returns the [4, B] float32 device buffer every
+        following step() updates -- running return, last finished episode's
+        return, its success (terminated 1, truncated 0), finished episodes --
+        or None when disabled."""
+        self._epstats = torch.zeros(4, self.num_envs, device=self.device) if enabled else None
+        self.sim._call("ps_set_episode_stats", self.sim._ctx, _ptr(self._epstats))
+        return self._epstats
 
     # ---------------------------------------------------------------- core
     def _obs_dict(self, obs=None, ag=None, dg=None):

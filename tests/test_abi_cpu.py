@@ -33,7 +33,7 @@ def test_library_exports_every_header_symbol(L):
 
 
 def test_abi_version(L):
-    assert L.lib().ps_abi_version() == 5
+    assert L.lib().ps_abi_version() == 6
 
 
 def test_state_layout(L):

@@ -156,3 +156,30 @@ def test_one_env_gymnasium_api(cls_name, env_id):
     # HER recomputes from the float32 goals of the observation; the step used
     # the float64 desired goal (as numpy does in the reference): rounding apart
     assert her.shape == (1,) and abs(float(her[0]) - r) <= 1e-6
+
+
+@pytest.mark.parametrize("lanes", [1, 8])
+def test_fused_episode_statistics_match_the_torch_ones(lanes):
+    """ps_set_episode_stats (RecordEpisodeStatistics inside the step kernel)
+    keeps the same bits as pandasim.dist.EpisodeStats updated from step()'s
+    outputs: running return, last return, last success, episode count, across
+    TimeLimit resets and successes."""
+    import pandasim
+    from pandasim.dist import EpisodeStats
+
+    B = 700
+    env = pandasim.make("PandaReachDense-v3", num_envs=B, lanes_per_env=lanes)
+    env.reset(seed=21)
+    fused = env.record_episode_statistics()
+    ref = EpisodeStats(B, "cuda")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(4)
+    for _ in range(120):
+        _, r, te, tr, _ = env.step(torch.rand(B, env.action_dim, device="cuda", generator=g) * 2 - 1, copy=False)
+        ref.update(r, te, tr)
+    assert torch.equal(fused[0], ref.running)
+    assert torch.equal(fused[1:], ref.packed())
+    assert int(fused[3].min()) >= 2  # at least the two TimeLimits
+    env.record_episode_statistics(False)
+    env.step(torch.zeros(B, env.action_dim, device="cuda"))
+    assert torch.equal(fused[1:], ref.packed())  # off: the buffer is left alone
