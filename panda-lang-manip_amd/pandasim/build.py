@@ -44,8 +44,10 @@ TASK_STACK = 4  # include/pandasim.h
 # Scheduler options of the one-lane step objects (scripts/build_variants.py
 # onelane_trk_clause, profiles/r03k_variants_sched.log): the AMDGPU register
 # pressure trackers, and memory-clause scheduling except for Stack -- every
-# task 0.3-0.9 % faster per step at 65 536 envs, Stack 2 %.  Scheduling only:
-# the arithmetic, and so every result, is unchanged.
+# task 0.3-0.9 % faster per step at 65 536 envs, Stack 2 %.  The group objects
+# take the trackers alone (groups_trk, profiles/r03k_variants_groups.log: 8-lane
+# Push/PickAndPlace at 8 192 envs 0.4 %, 16-lane at 4 096 2.7 %; memory-clause
+# scheduling was slower there).  Scheduling only: the arithmetic is unchanged.
 _SCHED = ["-mllvm", "-amdgpu-use-amdgpu-trackers"]
 _CLAUSE = ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]
 
@@ -60,7 +62,7 @@ UNITS = ([("pandasim", "pandasim.hip", [])]
              + _one_lane_flags(t))
             for t in range(6) for c in range(2)]
          + [(f"step_t{t}_c{c}_groups", "step_kernels.hip",
-             [f"-DPS_STEP_TASK={t}", f"-DPS_STEP_CONTROL={c}", "-DPS_STEP_GROUPS=1", "-O1"])
+             [f"-DPS_STEP_TASK={t}", f"-DPS_STEP_CONTROL={c}", "-DPS_STEP_GROUPS=1", "-O1"] + _SCHED)
             for t in range(6) if t != TASK_STACK for c in range(2)]
          + [(f"sim_{n}_{s}", "sim_kernels.hip", [f"-DPS_SIM_NOBJ={n}", f"-DPS_SIM_SHAPE={s}"])
             for n, s in ((0, 0), (1, 0), (1, 1), (2, 0))])

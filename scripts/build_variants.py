@@ -48,6 +48,10 @@ UNIT_VARIANTS = {
     # scheduler options on the one-lane step objects only
     "onelane_trk": lambda units: _one_lane(units, lambda t: _TRK),
     "onelane_trk_clause": lambda units: _one_lane(units, lambda t: _TRK + (_CLAUSE if t != 4 else [])),
+    # scheduler options on the -O1 group objects too
+    "groups_trk": lambda units: [(n, s, defs + (_TRK if n.endswith("_groups") else [])) for n, s, defs in units],
+    "groups_trk_clause": lambda units: [(n, s, defs + (_TRK + _CLAUSE if n.endswith("_groups") else []))
+                                        for n, s, defs in units],
     # the product before r03k: no scheduler options on the one-lane objects
     "onelane_plain": lambda units: [(n, s, [d for d in defs if d not in _TRK + _CLAUSE]) for n, s, defs in units],
     # the group-kernel objects at the library's -O3 (the product builds them at
