@@ -52,6 +52,15 @@ UNIT_VARIANTS = {
     "groups_trk": lambda units: [(n, s, defs + (_TRK if n.endswith("_groups") else [])) for n, s, defs in units],
     "groups_trk_clause": lambda units: [(n, s, defs + (_TRK + _CLAUSE if n.endswith("_groups") else []))
                                         for n, s, defs in units],
+    # further scheduler options on the one-lane objects (on top of the product's)
+    "onelane_iterilp": lambda units: _one_lane(units, lambda t: _TRK + ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]),
+    "onelane_itermin": lambda units: _one_lane(units, lambda t: _TRK + ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"]),
+    "onelane_clause_nu": lambda units: _one_lane(units, lambda t: _TRK + (_CLAUSE if t != 4 else []) + [
+        "-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule"]),
+    "onelane_greedyrev": lambda units: _one_lane(units, lambda t: _TRK + (_CLAUSE if t != 4 else []) + [
+        "-mllvm", "-greedy-reverse-local-assignment"]),
+    "onelane_mix": lambda units: _one_lane(units, lambda t: _TRK + (
+        _CLAUSE + ["-mllvm", "-greedy-reverse-local-assignment"] if t != 4 else [])),
     # the product before r03k: no scheduler options on the one-lane objects
     "onelane_plain": lambda units: [(n, s, [d for d in defs if d not in _TRK + _CLAUSE]) for n, s, defs in units],
     # the group-kernel objects at the library's -O3 (the product builds them at
