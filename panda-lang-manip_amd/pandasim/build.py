@@ -52,8 +52,16 @@ _SCHED = ["-mllvm", "-amdgpu-use-amdgpu-trackers"]
 _CLAUSE = ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]
 
 
+# greedy register allocation in reverse local order: Reach 1.3 %, Slide 1.0 %,
+# Push 0.6 % faster (three interleaved runs, profiles/r03k_variants_mix.log);
+# PickAndPlace and Flip unchanged, Stack 5 % slower
+_REVERSE = ["-mllvm", "-greedy-reverse-local-assignment"]
+
+
 def _one_lane_flags(task: int) -> list:
-    return _SCHED + (_CLAUSE if task != TASK_STACK else [])
+    if task == TASK_STACK:
+        return _SCHED
+    return _SCHED + _CLAUSE + (_REVERSE if task in (0, 1, 3) else [])
 
 
 # (object name, source, defines and per-unit flags)
