@@ -61,6 +61,12 @@ UNIT_VARIANTS = {
         "-mllvm", "-greedy-reverse-local-assignment"]),
     "onelane_mix": lambda units: _one_lane(units, lambda t: _TRK + (
         _CLAUSE + ["-mllvm", "-greedy-reverse-local-assignment"] if t != 4 else [])),
+    "groups_rev": lambda units: [(n, s, defs + (["-mllvm", "-greedy-reverse-local-assignment"]
+                                                if n.endswith("_groups") else [])) for n, s, defs in units],
+    "stack_itermin": lambda units: [(n, s, defs + (["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"]
+                                                   if n.startswith("step_t4_") else [])) for n, s, defs in units],
+    "stack_nu": lambda units: [(n, s, defs + (["-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule"]
+                                              if n.startswith("step_t4_") else [])) for n, s, defs in units],
     # the product before r03k: no scheduler options on the one-lane objects
     "onelane_plain": lambda units: [(n, s, [d for d in defs if d not in _TRK + _CLAUSE]) for n, s, defs in units],
     # the group-kernel objects at the library's -O3 (the product builds them at
