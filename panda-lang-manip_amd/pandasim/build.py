@@ -59,7 +59,9 @@ _REVERSE = ["-mllvm", "-greedy-reverse-local-assignment"]
 
 
 # Stack: the iterative minimum-register scheduler, 0.7 % faster (two
-# interleaved runs, profiles/r03k_variants_last.log)
+# interleaved runs, profiles/r03k_variants_last.log); also Reach's group
+# objects: C2 (Reach, 4 096 envs, 16 lanes) 2.2 % faster, while the 8-lane
+# Push/PickAndPlace objects got 1 % slower (profiles/r03k_variants_groups2.log)
 _MINREG = ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"]
 
 
@@ -75,7 +77,8 @@ UNITS = ([("pandasim", "pandasim.hip", [])]
              + _one_lane_flags(t))
             for t in range(6) for c in range(2)]
          + [(f"step_t{t}_c{c}_groups", "step_kernels.hip",
-             [f"-DPS_STEP_TASK={t}", f"-DPS_STEP_CONTROL={c}", "-DPS_STEP_GROUPS=1", "-O1"] + _SCHED)
+             [f"-DPS_STEP_TASK={t}", f"-DPS_STEP_CONTROL={c}", "-DPS_STEP_GROUPS=1", "-O1"] + _SCHED
+             + (_MINREG if t == 0 else []))
             for t in range(6) if t != TASK_STACK for c in range(2)]
          + [(f"sim_{n}_{s}", "sim_kernels.hip", [f"-DPS_SIM_NOBJ={n}", f"-DPS_SIM_SHAPE={s}"])
             for n, s in ((0, 0), (1, 0), (1, 1), (2, 0))])

@@ -67,6 +67,12 @@ UNIT_VARIANTS = {
                                                    if n.startswith("step_t4_") else [])) for n, s, defs in units],
     "stack_nu": lambda units: [(n, s, defs + (["-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule"]
                                               if n.startswith("step_t4_") else [])) for n, s, defs in units],
+    "groups_maxilp": lambda units: [(n, s, defs + (["-mllvm", "-amdgpu-sched-strategy=max-ilp"]
+                                                   if n.endswith("_groups") else [])) for n, s, defs in units],
+    "groups_minreg": lambda units: [(n, s, defs + (["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"]
+                                                   if n.endswith("_groups") else [])) for n, s, defs in units],
+    "groups_nu": lambda units: [(n, s, defs + (["-mllvm", "-amdgpu-disable-unclustered-high-rp-reschedule"]
+                                               if n.endswith("_groups") else [])) for n, s, defs in units],
     # the product before r03k: no scheduler options on the one-lane objects
     "onelane_plain": lambda units: [(n, s, [d for d in defs if d not in _TRK + _CLAUSE]) for n, s, defs in units],
     # the group-kernel objects at the library's -O3 (the product builds them at
