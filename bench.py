@@ -198,17 +198,38 @@ def fp32_roofline(work: dict, n_objects: int, env_steps_per_s_per_gpu: float) ->
                      "and the PGS runs to the wave's slowest env (the counts are each env's own)")
 
 
-def load_pmc(workload: str, key: str = "bytes_per_launch"):
-    """Per-launch PMC figures of k_step for `workload` from the committed
-    rocprofv3 summary (profiles/pmc_traffic.json, scripts/summarize_profiles.py)."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if not os.path.exists(path):
+def file_sha256(path: str):
+    import hashlib
+
+    try:
+        h = hashlib.sha256()
+        with open(path, "rb") as f:
+            for chunk in iter(lambda: f.read(1 << 20), b""):
+                h.update(chunk)
+        return h.hexdigest()
+    except OSError:
         return None
+
+
+def pmc_entry(workload: str, lib_path: str, path: str | None = None):
+    """The committed rocprofv3 PMC figures of k_step for `workload`
+    (profiles/pmc_traffic.json, scripts/summarize_profiles.py) and their
+    status.  They describe one binary: the entry records the sha256 of the
+    libpandasim.so it was measured on, and it is used only when that equals
+    the hash of the library this process loaded ("current"); otherwise
+    ("stale", or "missing") the PMC-derived fields are left out of the line."""
+    path = path or os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         entry = json.load(open(path)).get(workload)
-        return None if entry is None else entry.get(key)
     except Exception:
-        return None
+        entry = None
+    lib_hash = file_sha256(lib_path)
+    if entry is None:
+        return None, {"status": "missing", "lib_sha256": lib_hash}
+    status = "current" if entry.get("lib_sha256") and entry.get("lib_sha256") == lib_hash else "stale"
+    info = {"status": status, "lib_sha256": lib_hash, "measured_on": entry.get("lib_sha256"),
+            "source": entry.get("source")}
+    return (entry if status == "current" else None), info
 
 
 def launch_command(n: int, argv) -> list:
@@ -329,6 +350,10 @@ def main():
     bytes_env = algorithmic_bytes_per_env_step(env.obs_dim, env.action_dim, env.goal_dim, env.sim.cfg.n_objects)
     achieved = bytes_env * B / (kernel_ms * 1e-3) / 1e9
     workload = f"{args.env_id} x{B}/gpu"
+    from pandasim import _lib as _L
+
+    pmc, pmc_info = pmc_entry(workload, _L.LIB_PATH)
+    pmc = pmc or {}
     out = {
         "metric": "env steps/sec (batched) PandaPush-v3 at 1/2/4/8 MI355X vs PyBullet CPU",
         "value": round(value, 1),
@@ -347,16 +372,16 @@ def main():
                    "global_batch": world * B, "substeps": 20, "parallelism": f"batch shard x{world}",
                    "lanes_per_env": env.lanes_per_env},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": load_pmc(workload),
+                     "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": pmc.get("bytes_per_launch"),
                      "kernel": f"k_step<{spec['task'].upper()},{spec['control_type'].upper()},{env.lanes_per_env}>",
                      "kernel_ms": round(kernel_ms, 4),
-                     "bytes_per_env_step": bytes_env},
+                     "bytes_per_env_step": bytes_env, "pmc": pmc_info},
     }
     # The binding limit is VALU issue, not HBM: one wave per
     # SIMD at 65 536 envs (1 024 waves on 1 024 SIMDs) issues at most one VALU
     # instruction per 4 cycles (MI355X_MICROARCH.md, 'vector-instruction ISSUE
     # cost'), two or more waves per SIMD one per 2 cycles.
-    valu = load_pmc(workload, "valu_insts_per_launch")
+    valu = pmc.get("valu_insts_per_launch")
     if valu:
         rate = valu / (kernel_ms * 1e-3)
         simds, clk = 256 * 4, 2.4e9
@@ -365,7 +390,7 @@ def main():
             "peak_one_wave_per_simd": round(simds * clk / 4 / 1e9, 2), "peak_dual_issue": round(simds * clk / 2 / 1e9, 2),
             "frac_one_wave_per_simd": round(rate / (simds * clk / 4), 4),
             "valu_insts_per_launch": valu, "source": "profiles/pmc_traffic.json (SQ_INSTS_VALU)"}
-    executed = load_pmc(workload, "fp32_flops_executed_per_launch")
+    executed = pmc.get("fp32_flops_executed_per_launch")
     if executed:
         rate = executed / (kernel_ms * 1e-3) / 1e12
         out["roofline"]["fp32_executed"] = {

@@ -194,10 +194,12 @@ int ps_set_nonfinite_guard(ps_ctx *ctx, uint8_t *flags, int reset_nonfinite);
  * control_joints, pybullet.py:462-477), as env.step does.  It stores the
  * motor targets and max impulses every step but the gain rows (kp, kd,
  * target velocity) only when they may differ from its own: on the first
- * ps_step after ps_create or ps_init_state, on a step of another state
- * buffer than the last step's, and after this call.  A caller that writes
- * motor rows of the same buffer itself (the plugin path's control_joints,
- * a raw write into the state, a snapshot copied into it) calls it first. */
+ * ps_step after ps_create, ps_init_state or ps_reset, and after this call
+ * (a step of a buffer at another address than the last step's also writes
+ * them, but a caching allocator can hand a new buffer the old address, so
+ * callers must not rely on that).  A caller that swaps buffers without a
+ * ps_reset, or writes motor rows itself (the plugin path's control_joints,
+ * a raw write into the state, a snapshot copied into it), calls it first. */
 int ps_mark_motor_rows_dirty(ps_ctx *ctx);
 
 /* Engine level: PyBullet.step() (pybullet.py:52-55) with the motors already in

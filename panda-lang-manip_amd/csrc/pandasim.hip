@@ -69,6 +69,10 @@ __global__ __launch_bounds__(kBlock) void k_reset(KParams P, const uint8_t *mask
     aux_rng(s, i) = aux;
     s.E(i) = 0;
     clear_contact_cache(s, i);
+    // RecordEpisodeStatistics (ps_set_episode_stats) zeroes the running
+    // return on reset(): an abandoned episode's partial return does not carry
+    // into the next one
+    if (P.epstats) P.epstats[i] = 0.0f;
     write_obs<TASK>(P, i, q, qd, bd, g, obs, ag, dg);
 }
 
@@ -691,6 +695,11 @@ int ps_reset(ps_ctx *c, void *state, const uint8_t *mask, const uint64_t *seeds,
     KParams P = params_of(c, state);
     dim3 g = grid_of(P.n, kBlock), b(kBlock);
     hipStream_t st = (hipStream_t)stream;
+    // the next step rewrites the gain rows: a reset is where a caller starts
+    // with a fresh or swapped-in buffer, whose address a caching allocator may
+    // have handed out before (so the pointer test of the step launcher alone
+    // would not see it)
+    c->gains_dirty = 1;
 #define PS_LAUNCH_RESET(T) hipLaunchKernelGGL(k_reset<T>, g, b, 0, st, P, mask, seeds, obs, ag, dg)
     switch (c->cfg.task) {
         case PS_TASK_REACH: PS_LAUNCH_RESET(PS_TASK_REACH); break;

@@ -53,6 +53,15 @@ class EpisodeStats:
         self.episodes.add_(done.to(torch.int32))
         self.running.masked_fill_(done, 0.0)
 
+    def reset(self, mask: Optional[torch.Tensor] = None) -> None:
+        """env.reset() (of every env, or of `mask`): the running return
+        restarts at 0, as gymnasium's RecordEpisodeStatistics does; the last
+        finished episode's figures stay."""
+        if mask is None:
+            self.running.zero_()
+        else:
+            self.running.masked_fill_(mask.to(self.running.device).bool(), 0.0)
+
     def packed(self) -> torch.Tensor:
         """[3, B] float32: last return, last success, episode count."""
         return torch.stack([self.last_return, self.last_success, self.episodes.to(torch.float32)])

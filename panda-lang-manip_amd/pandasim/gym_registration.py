@@ -116,16 +116,28 @@ def registrations():
     return out
 
 
-def register_envs() -> list:
-    """Register the 24 IDs with gymnasium (skips IDs already registered);
-    returns the IDs.  Raises ImportError when gymnasium is not installed."""
+def register_envs(override: bool = False) -> list:
+    """Register the 24 IDs with gymnasium; returns the IDs.  An ID already
+    registered with pandasim's entry point is kept.  One registered by
+    another package (panda_gym imported first: gym.make would build the
+    reference's PyBullet env) raises RuntimeError, unless ``override=True``,
+    which re-registers it to pandasim.  Raises ImportError when gymnasium is
+    not installed."""
     if _gym is None:
         raise ImportError("gymnasium is not installed: pandasim.make(env_id, num_envs) needs no registry")
     from gymnasium.envs.registration import register, registry
 
     ids = []
     for env_id, entry_point, kwargs, steps in registrations():
-        if env_id not in registry:
-            register(id=env_id, entry_point=entry_point, kwargs=kwargs, max_episode_steps=steps)
+        if env_id in registry:
+            theirs = registry[env_id].entry_point
+            if theirs == entry_point:
+                ids.append(env_id)
+                continue
+            if not override:
+                raise RuntimeError(f"{env_id} is already registered to {theirs!r} (panda_gym imported first?); "
+                                   "call register_envs(override=True) to point it at pandasim")
+            del registry[env_id]
+        register(id=env_id, entry_point=entry_point, kwargs=kwargs, max_episode_steps=steps)
         ids.append(env_id)
     return ids

@@ -22,6 +22,7 @@ from __future__ import annotations
 import argparse
 import collections
 import csv
+import hashlib
 import json
 import os
 import shutil
@@ -77,6 +78,8 @@ def main():
     ap.add_argument("--steps", type=int, default=100, help="timed launches at the tail of the trace")
     ap.add_argument("--kernel", default="k_step")
     ap.add_argument("--prefix", default="prof")
+    ap.add_argument("--lib", default=os.path.join(ROOT, "panda-lang-manip_amd", "pandasim", "libpandasim.so"),
+                    help="the library the profiled run loaded (its sha256 goes into pmc_traffic.json)")
     args = ap.parse_args()
     os.makedirs(PROF, exist_ok=True)
     tdir = os.path.join(OUT, f"{args.prefix}_trace")
@@ -135,8 +138,14 @@ def main():
     if step and "hbm_bytes_per_launch" in kernels[step[0]]:
         tpath = os.path.join(PROF, "pmc_traffic.json")
         traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
+        # the binary the counters describe: bench.py uses the entry only while
+        # the library it loads has this hash
+        lib_hash = hashlib.sha256(open(args.lib, "rb").read()).hexdigest()
         traffic[args.workload] = {"bytes_per_launch": round(kernels[step[0]]["hbm_bytes_per_launch"]),
-                                  "source": f"profiles/{args.tag}_summary.json", "fetch_factor": factor}
+                                  "source": f"profiles/{args.tag}_summary.json", "fetch_factor": factor,
+                                  "lib_sha256": lib_hash}
+        summary["lib_sha256"] = lib_hash
+        json.dump(summary, open(os.path.join(PROF, f"{args.tag}_summary.json"), "w"), indent=1)
         sq = kernels[step[0]].get("sq_counters_per_launch", {})
         if "SQ_INSTS_VALU" in sq:
             traffic[args.workload]["valu_insts_per_launch"] = round(sq["SQ_INSTS_VALU"])

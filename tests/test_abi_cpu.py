@@ -130,11 +130,12 @@ def test_bench_algorithmic_bytes_and_pmc_entries():
     # + the contact cache: 10 rows read and written (ground of the cube, gripper)
     assert bench.algorithmic_bytes_per_env_step(obs_dim=18, action_dim=3) == 630  # PandaPush-v3
     assert bench.algorithmic_bytes_per_env_step(obs_dim=6, action_dim=3, n_objects=0) == 390  # PandaReach-v3
-    traffic = bench.load_pmc("PandaPush-v3 x65536/gpu")
-    assert traffic is None or traffic > 0
-    valu = bench.load_pmc("PandaPush-v3 x65536/gpu", "valu_insts_per_launch")
-    assert valu is None or valu > 1e8
-    assert bench.load_pmc("no such workload") is None
+    entry, info = bench.pmc_entry("PandaPush-v3 x65536/gpu", os.path.join(ROOT, "panda-lang-manip_amd", "pandasim",
+                                                                         "libpandasim.so"))
+    assert info["status"] in ("current", "stale", "missing")
+    if entry is not None:  # measured on the library in the tree
+        assert entry["bytes_per_launch"] > 0 and entry.get("valu_insts_per_launch", 1e9) > 1e8
+    assert bench.pmc_entry("no such workload", __file__)[0] is None
 
 
 def test_flop_model_counts():

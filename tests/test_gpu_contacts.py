@@ -403,6 +403,65 @@ def test_reach_at_config_size():
             assert np.abs(og[i, 3:6] - o[3:6]).max() < 2e-3, (control, i)
 
 
+@pytest.mark.parametrize("task", ["push", "pick_and_place"])
+def test_push_and_pick_and_place_at_config_size(task):
+    """BASELINE configs C3 (PandaPush-v3) and C4 (PandaPickAndPlace-v3) at
+    their own size, 8 192 envs, on the kernel the library picks for it
+    (lanes_per_env = 0 resolves to the 8-lane group kernel): 60 autoreset
+    steps with finite, bounded observations and exact TimeLimit bookkeeping,
+    then 3 steps of 64 evenly spaced envs teacher-forced against the oracle
+    at the tight bounds of test_env_step_parity_teacher_forced.  PickAndPlace
+    (free gripper) holds the samples the oracle itself cannot resolve at fp32
+    resolution (finger-limit branches: _ill_conditioned) to the loose bounds
+    instead, at most 8 % of them."""
+    from test_gpu_parity import FREE_GRIPPER, LOOSE, TOL, _groups, _ill_conditioned, _within
+
+    from pandasim.envs import PandaVecEnv
+
+    B = 8192
+    env = PandaVecEnv(task, "sparse", "ee", B, "cuda", lanes_per_env=0)
+    assert env.lanes_per_env == 8
+    env.autoreset = True
+    env.reset(seed=2024)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(17)
+    steps_in_episode = torch.zeros(B, dtype=torch.int64, device="cuda")
+    for s in range(60):
+        obs, r, te, tr, info = env.step(torch.rand(B, env.action_dim, device="cuda", generator=g) * 2 - 1)
+        steps_in_episode += 1
+        assert torch.equal(tr, steps_in_episode == env.max_episode_steps)
+        steps_in_episode[te | tr] = 0
+        assert torch.isfinite(obs["observation"]).all()
+        assert (obs["observation"].abs() < 100).all()
+    assert torch.equal(env.sim.elapsed[:B].long(), steps_in_episode)
+    env.autoreset = False
+    cfg = oracle_config_for(env.sim.cfg)
+    groups = _groups(task, 7 if task in FREE_GRIPPER else 6)
+    tol = TOL[task]
+    sample = np.linspace(0, B - 1, 64).astype(int)
+    worst = {k: 0.0 for k in groups}
+    n_bif = 0
+    for s in range(3):
+        snap = snapshot(env.sim)
+        a = torch.rand(B, env.action_dim, device="cuda", generator=g) * 2 - 1
+        obs, r, te, tr, _ = env.step(a)
+        og, a = obs["observation"].cpu().numpy(), a.cpu().numpy()
+        te, tr = te.cpu().numpy(), tr.cpu().numpy()
+        for i in sample:
+            o, ag, dg, rr, t_e, t_r = O.step(cfg, oracle_env_from(cfg, snap, i), a[i])
+            assert t_r == bool(tr[i]), (s, i)
+            bif = task in FREE_GRIPPER and _ill_conditioned(cfg, snap, i, a[i], o, groups, tol)
+            n_bif += bif
+            for k, idx in groups.items():
+                err = float(np.abs(og[i, idx] - o[idx]).max())
+                assert _within(err, o[idx], k, LOOSE if bif else tol), (task, s, i, k, err, bif)
+                if not bif:
+                    worst[k] = max(worst[k], err)
+    print(task, f"{B} envs, 8 lanes:", {k: f"{v:.1e}" for k, v in worst.items()},
+          f"ill-conditioned {n_bif}/{3 * len(sample)}")
+    assert n_bif <= 0.08 * 3 * len(sample)
+
+
 def test_bench_config_after_60_steps():
     """The bench's exact workload (PandaPush-v3, 65 536 envs, ee, autoreset)
     after 60 steps -- past the first TimeLimit, mid-episode contacts in the

@@ -183,3 +183,44 @@ def test_fused_episode_statistics_match_the_torch_ones(lanes):
     env.record_episode_statistics(False)
     env.step(torch.zeros(B, env.action_dim, device="cuda"))
     assert torch.equal(fused[1:], ref.packed())  # off: the buffer is left alone
+
+
+@pytest.mark.parametrize("lanes", [1, 8])
+def test_fused_episode_statistics_restart_on_reset(lanes):
+    """An explicit reset() mid-episode -- of every env and of a masked subset
+    -- zeroes the running return (k_reset), as gymnasium's
+    RecordEpisodeStatistics does: the abandoned episode's partial return does
+    not carry into the next one.  Compared bit for bit with EpisodeStats whose
+    running return is cleared on the same resets."""
+    import pandasim
+    from pandasim.dist import EpisodeStats
+
+    B = 300
+    env = pandasim.make("PandaPushDense-v3", num_envs=B, lanes_per_env=lanes)
+    env.reset(seed=5)
+    fused = env.record_episode_statistics()
+    ref = EpisodeStats(B, "cuda")
+    g = torch.Generator(device="cuda")
+    g.manual_seed(9)
+    mask = torch.zeros(B, dtype=torch.bool, device="cuda")
+    mask[::3] = True
+
+    def steps(n):
+        for _ in range(n):
+            _, r, te, tr, _ = env.step(torch.rand(B, env.action_dim, device="cuda", generator=g) * 2 - 1,
+                                       copy=False)
+            ref.update(r, te, tr)
+
+    steps(7)
+    assert float((fused[0][mask] != 0).float().mean()) > 0.9  # mid-episode (a few may have just succeeded)
+    env.reset(mask=mask)
+    ref.reset(mask)
+    assert torch.equal(fused[0][mask], torch.zeros(int(mask.sum()), device="cuda"))
+    assert torch.equal(fused[0], ref.running)
+    steps(60)  # across a TimeLimit of the un-reset envs
+    env.reset()
+    ref.reset()
+    assert not fused[0].any()
+    steps(5)
+    assert torch.equal(fused[0], ref.running)
+    assert torch.equal(fused[1:], ref.packed())

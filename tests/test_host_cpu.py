@@ -189,6 +189,7 @@ def test_gymnasium_registration_mirrors_the_reference(monkeypatch):
     gymnasium -- checked against a stand-in registry, as gymnasium is not
     installed in this image."""
     import importlib
+    import importlib.util
     import sys
     import types
 
@@ -201,7 +202,7 @@ def test_gymnasium_registration_mirrors_the_reference(monkeypatch):
 
     def register(id, entry_point, kwargs, max_episode_steps):
         calls.append((id, entry_point, kwargs, max_episode_steps))
-        reg_mod.registry[id] = entry_point
+        reg_mod.registry[id] = types.SimpleNamespace(entry_point=entry_point)  # gymnasium's EnvSpec field
 
     reg_mod.register = register
     gym.envs = envs_mod
@@ -231,8 +232,48 @@ def test_gymnasium_registration_mirrors_the_reference(monkeypatch):
         n = len(calls)
         GR.register_envs()
         assert len(calls) == n
+        # an ID another package registered (panda_gym imported first) is not
+        # silently kept: it raises, and override=True points it at pandasim
+        reg_mod.registry["PandaPush-v3"] = types.SimpleNamespace(entry_point="panda_gym.envs:PandaPushEnv")
+        with pytest.raises(RuntimeError, match="panda_gym"):
+            GR.register_envs()
+        GR.register_envs(override=True)
+        assert reg_mod.registry["PandaPush-v3"].entry_point == "pandasim.gym_registration:PandaPushGymEnv"
+        assert len(calls) == n + 1
     finally:
         monkeypatch.undo()
         importlib.reload(GR)
-    with pytest.raises(ImportError):
-        GR.register_envs()
+    if importlib.util.find_spec("gymnasium") is None:
+        with pytest.raises(ImportError):
+            GR.register_envs()
+
+
+def test_bench_pmc_fields_are_tied_to_the_binary(tmp_path):
+    """bench.py takes roofline.traffic, valu_issue and fp32_executed from the
+    committed PMC summary only while the library it loaded is the binary the
+    counters were measured on (the sha256 summarize_profiles.py records);
+    a mismatched or absent hash leaves the fields out ("stale")."""
+    import importlib.util
+    import json
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(root, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    lib = tmp_path / "libpandasim.so"
+    lib.write_bytes(b"\x7fELF built once")
+    good = bench.file_sha256(str(lib))
+    entry = {"bytes_per_launch": 45_000_000, "valu_insts_per_launch": 10**9, "source": "profiles/x_summary.json"}
+    pmc = tmp_path / "pmc_traffic.json"
+    pmc.write_text(json.dumps({"W": dict(entry, lib_sha256=good), "V": dict(entry, lib_sha256="0" * 64),
+                               "U": entry}))
+    e, info = bench.pmc_entry("W", str(lib), str(pmc))
+    assert info["status"] == "current" and e["bytes_per_launch"] == 45_000_000
+    for w in ("V", "U"):  # measured on another binary, or on an unrecorded one
+        e, info = bench.pmc_entry(w, str(lib), str(pmc))
+        assert e is None and info["status"] == "stale"
+    e, info = bench.pmc_entry("absent", str(lib), str(pmc))
+    assert e is None and info["status"] == "missing"
+    lib.write_bytes(b"\x7fELF rebuilt")  # the library changed after the profile
+    e, info = bench.pmc_entry("W", str(lib), str(pmc))
+    assert e is None and info["status"] == "stale" and info["measured_on"] == good
