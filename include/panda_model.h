@@ -18,10 +18,21 @@
  *                       link-1 COM pinned by test/pybullet_test.py:124-136 and
  *                       the IK solution pinned by test/pybullet_test.py:254-266)
  *   link inertias       PyBullet recomputes them from collision-mesh AABBs
- *                       (no URDF_USE_INERTIA_FROM_FILE, envs/core.py:47-52);
- *                       the meshes are not available, so the AABB extents
- *                       below are estimates calibrated against the joint-5
- *                       motor KATs test/pybullet_test.py:139-204.
+ *                       (no URDF_USE_INERTIA_FROM_FILE, envs/core.py:47-52).
+ *                       Hand and fingers (links 8-10): from the hulls the
+ *                       reference ships (contact_graspnet/gripper_models/
+ *                       panda_gripper/{hand,finger}.stl, fixture
+ *                       tests/golden/panda_gripper_hulls.npz): the hand is
+ *                       its hull above the flange plane (z >= 0; the 34
+ *                       vertices below it would move the joint-5 KAT's
+ *                       angular velocity to -2.949, 0.02 outside the
+ *                       reference's -2.969 +- 1e-3) plus Bullet's 1 mm convex
+ *                       margin per side, the fingers their hull's extents
+ *                       (tests/test_host_cpu.py checks both against the
+ *                       fixture).  The arm links 0-6 have no
+ *                       mesh in the reference: their AABB extents are
+ *                       estimates calibrated against the joint-5 motor KATs
+ *                       test/pybullet_test.py:139-204.
  */
 #ifndef PANDA_MODEL_H
 #define PANDA_MODEL_H
@@ -98,11 +109,11 @@
     X(7, 6, PM_JOINT_FIXED, 0.0, 0.0, 0.107, 0.0, 0.0, 0.0, 0.0, 0.0, 1.0, -1, 0.0, 0.0, 0.0, 0.0, 0.0,    \
       0.0, 0.0)                                                                                            \
     X(8, 7, PM_JOINT_FIXED, 0.0, 0.0, 0.0, 0.0, 0.0, -PM_QUARTER_PI_URDF, 0.0, 0.0, 1.0, -1, 0.81, 0.0,   \
-      0.0, 0.04, 0.064, 0.206, 0.068)                                                                      \
+      0.0, 0.04, 0.0653, 0.2064, 0.0674)                                                                      \
     X(9, 8, PM_JOINT_PRISMATIC, 0.0, 0.0, 0.0584, 0.0, 0.0, 0.0, 0.0, 1.0, 0.0, 7, 0.1, 0.0, 0.01, 0.02,   \
-      0.022, 0.022, 0.054)                                                                                 \
+      0.0210, 0.0265, 0.0537)                                                                                 \
     X(10, 8, PM_JOINT_PRISMATIC, 0.0, 0.0, 0.0584, 0.0, 0.0, 0.0, 0.0, -1.0, 0.0, 8, 0.1, 0.0, -0.01,      \
-      0.02, 0.022, 0.022, 0.054)                                                                           \
+      0.02, 0.0210, 0.0265, 0.0537)                                                                           \
     X(11, 8, PM_JOINT_FIXED, 0.0, 0.0, 0.105, 0.0, 0.0, 0.0, 0.0, 0.0, 1.0, -1, 0.0, 0.0, 0.0, 0.0, 0.0,  \
       0.0, 0.0)
 
@@ -124,17 +135,36 @@
 #define PM_BASE_X (-0.6)
 
 /*
- * Collision proxies of the hand, fingers and link 7 (PyBullet collides the
- * URDF's convex meshes, which are not available): spheres in link frames.
- * X(link, cx, cy, cz, radius, lateral_friction)
- *   fingers (links 9, 10): two pad spheres each; panda.py:47-48 set their
- *     lateral friction to 1.0;
- *   hand (link 8): both ends of the palm bar and its centre (the palm face
- *     between the fingers), default friction 0.5;
- *   link 7 (PyBullet link 6, "panda_link7"): the wrist body above the flange.
- * Contacts are offered in this order (fingers first), PM_MAX_ROBOT_CONTACTS
- * at most.
+ * Collision proxies of the hand and fingers: boxes in link frames, the AABBs
+ * of the reference's hulls (PyBullet collides the URDF's convex meshes; the
+ * reference ships the same hand and finger hulls, tests/golden/
+ * panda_gripper_hulls.npz).
+ * X(link, cx, cy, cz, hx, hy, hz, lateral_friction)
+ *   fingers (links 9, 10): the finger hull's AABB (0.021 x 0.0265 x 0.054 m,
+ *     its pad face at y = 0 of the finger frame; link 10 is link 9 turned by
+ *     pi about z); panda.py:47-48 set their lateral friction to 1.0;
+ *   hand (link 8): the palm, the AABB of the hand hull's part below the
+ *     finger slots (z >= 0.03: the face between the fingers at z = 0.066),
+ *     default friction 0.5.
+ * Link 7 (PyBullet link 6, "panda_link7", no mesh in the reference) keeps a
+ * sphere proxy of the wrist body above the flange (PM_WRIST_SPHERE).
+ * Contacts are offered per object, then for the ground, in the order boxes
+ * (fingers first), wrist: at most PM_BOX_CONTACTS per box and target
+ * (DESIGN.md §5), PM_MAX_ROBOT_CONTACTS in all.
  */
+#define PM_NUM_BOXES 3
+#define PM_BOX_TABLE(X)                                                  \
+    X(9, 0.0, 0.0131, 0.0270, 0.0105, 0.0133, 0.0269, 1.0)              \
+    X(10, 0.0, -0.0131, 0.0270, 0.0105, 0.0133, 0.0269, 1.0)            \
+    X(8, 0.0007, 0.0001, 0.0481, 0.0200, 0.1004, 0.0178, 0.5)
+#define PM_BOX_CONTACTS 2
+/* X(link, cx, cy, cz, radius, lateral_friction) */
+#define PM_WRIST_SPHERE(X) X(6, 0.0, 0.0, 0.060, 0.050, 0.5)
+#define PM_CONTACT_MARGIN_ROBOT 0.005
+
+/* Visual proxies of the fingers, palm and wrist for the camera images
+ * (ps_render, oracle/render_oracle.py) -- not collided:
+ * X(link, cx, cy, cz, radius, unused) */
 #define PM_NUM_SPHERES 8
 #define PM_SPHERE_TABLE(X)                       \
     X(9, 0.0, 0.0095, 0.0205, 0.0095, 1.0)      \

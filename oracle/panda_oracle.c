@@ -808,26 +808,369 @@ static void box_box_contacts(const po_config *cfg, const po_env *env, const oobj
     }
 }
 
+/* ------------------------------------------------ gripper collision boxes
+ * The hand and finger hulls (panda_model.h PM_BOX_TABLE: AABBs of the
+ * reference's hand.stl / finger.stl) against the objects and the ground.
+ * Each (box, target) pair yields at most PM_BOX_CONTACTS points, chosen from
+ * a fixed candidate set (Bullet clips hull against hull,
+ * btPolyhedralContactClipping, and keeps up to 4 points per manifold; the
+ * candidates below are the vertices of that clipped polygon, enumerated
+ * without building it):
+ *   box vs cube: separating axis over the 6 face normals (least penetration,
+ *     earlier axis on ties) gives the reference face and its normal; the
+ *     candidates are the incident face's 4 vertices inside the reference
+ *     rectangle, the rectangle's 4 corners inside the incident face, and the
+ *     16 crossings of their edges, at their depths below the reference face;
+ *   box vs cylinder (Slide): the box's 8 vertices against the solid
+ *     (object_closest), for every side face of the box the cylinder's
+ *     generator line facing it clipped to the face (a line contact of a face
+ *     on the curved side: its two ends), and the cylinder's 16 rim points
+ *     against the box;
+ *   box vs ground: the box's 8 vertices.
+ * Of the candidates within PM_CONTACT_MARGIN_ROBOT the deepest is taken, then
+ * the one farthest from it (0.1 mm apart at least); the two are ordered along
+ * the box's longest axis, which makes the order (the contact's cache id) a
+ * property of the geometry.  A is the robot, B the object or ground, n points
+ * from B to A. */
+typedef struct {
+    double pA[3], pB[3], n[3], dist;
+} ocand;
+
+typedef struct {
+    int link;
+    double c[3], h[3], mu;
+} obox_def;
+
+static const obox_def BOXES[PM_NUM_BOXES] = {
+#define OL_BOX(link_, cx, cy, cz, hx, hy, hz, mu_) {link_, {cx, cy, cz}, {hx, hy, hz}, mu_},
+    PM_BOX_TABLE(OL_BOX)
+#undef OL_BOX
+};
+
+/* world pose of box b: centre, rotation (columns = box axes) */
+static void robot_box(const okin *k, int b, double c[3], double R[9]) {
+    const obox_def *d = &BOXES[b];
+    double t[3];
+    m3_vec(k->R[d->link], d->c, t);
+    for (int j = 0; j < 3; j++) c[j] = k->o[d->link][j] + t[j];
+    memcpy(R, k->R[d->link], sizeof(double) * 9);
+}
+
+static int longest_axis(const double h[3]) { return h[2] >= h[1] && h[2] >= h[0] ? 2 : (h[1] >= h[0] ? 1 : 0); }
+
+static int pick_contacts(const ocand *cand, int m, const double bc[3], const double bR[9], int ax, ocand out[2]) {
+    int first = -1;
+    for (int i = 0; i < m; i++)
+        if (cand[i].dist < PM_CONTACT_MARGIN_ROBOT && (first < 0 || cand[i].dist < cand[first].dist)) first = i;
+    if (first < 0) return 0;
+    int second = -1;
+    double best = 1e-8; /* (0.1 mm)^2 */
+    for (int i = 0; i < m; i++) {
+        if (i == first || !(cand[i].dist < PM_CONTACT_MARGIN_ROBOT)) continue;
+        double d2 = 0.0;
+        for (int j = 0; j < 3; j++) d2 += (cand[i].pA[j] - cand[first].pA[j]) * (cand[i].pA[j] - cand[first].pA[j]);
+        if (d2 > best) { best = d2; second = i; }
+    }
+    out[0] = cand[first];
+    if (second < 0) return 1;
+    out[1] = cand[second];
+    double axis[3] = {bR[ax], bR[3 + ax], bR[6 + ax]}, r0[3], r1[3];
+    for (int j = 0; j < 3; j++) { r0[j] = out[0].pA[j] - bc[j]; r1[j] = out[1].pA[j] - bc[j]; }
+    if (v3_dot(r1, axis) < v3_dot(r0, axis)) {
+        ocand t = out[0];
+        out[0] = out[1];
+        out[1] = t;
+    }
+    return 2;
+}
+
+/* robot box (centre xc, rotation xR, half xh) vs the cube i */
+static int box_cube_cands(const double xc[3], const double xR[9], const double xh[3], const double yc[3],
+                          const double yR[9], const double yh[3], ocand *cand) {
+    const double *cen[2] = {xc, yc}, *rot[2] = {xR, yR}, *hh[2] = {xh, yh};
+    double d[3] = {yc[0] - xc[0], yc[1] - xc[1], yc[2] - xc[2]};
+    double best = 1e30, nref[3] = {0, 0, 0};
+    int ref = 0, axn = 0;
+    for (int b = 0; b < 2; b++)
+        for (int ax = 0; ax < 3; ax++) {
+            double L[3] = {rot[b][ax], rot[b][3 + ax], rot[b][6 + ax]};
+            double ra = 0.0, rb = 0.0;
+            for (int j = 0; j < 3; j++) {
+                ra += xh[j] * fabs(xR[j] * L[0] + xR[3 + j] * L[1] + xR[6 + j] * L[2]);
+                rb += yh[j] * fabs(yR[j] * L[0] + yR[3 + j] * L[1] + yR[6 + j] * L[2]);
+            }
+            double c = v3_dot(d, L);
+            double pen = ra + rb - fabs(c);
+            if (pen < -PM_CONTACT_MARGIN_ROBOT) return 0;
+            if (pen < best - PM_PAIR_AXIS_TOL) {
+                best = pen;
+                ref = b;
+                axn = ax;
+                double sg = (b == 0 ? c : -c) >= 0.0 ? 1.0 : -1.0; /* from the reference toward the incident box */
+                for (int j = 0; j < 3; j++) nref[j] = L[j] * sg;
+            }
+        }
+    int inc = 1 - ref;
+    const double *Rr = rot[ref], *Ri = rot[inc], *hr = hh[ref], *hi = hh[inc];
+    int a1 = (axn + 1) % 3, a2 = (axn + 2) % 3;
+    double t1[3] = {Rr[a1], Rr[3 + a1], Rr[6 + a1]}, t2[3] = {Rr[a2], Rr[3 + a2], Rr[6 + a2]};
+    double cf[3];
+    for (int j = 0; j < 3; j++) cf[j] = cen[ref][j] + nref[j] * hr[axn];
+    double hu = hr[a1], hv = hr[a2];
+    /* incident face: the incident box's axis most anti-parallel to nref */
+    int ai = 0;
+    double mostneg = 2.0, si = 1.0;
+    for (int ax = 0; ax < 3; ax++) {
+        double L[3] = {Ri[ax], Ri[3 + ax], Ri[6 + ax]};
+        double dn = v3_dot(L, nref);
+        if (-fabs(dn) < mostneg) { mostneg = -fabs(dn); ai = ax; si = dn > 0.0 ? -1.0 : 1.0; }
+    }
+    int b1 = (ai + 1) % 3, b2 = (ai + 2) % 3;
+    static const double cu[4] = {-1, 1, 1, -1}, cv[4] = {-1, -1, 1, 1};
+    double P[4][3]; /* incident face vertices in (u, v, depth) */
+    for (int q = 0; q < 4; q++) {
+        double loc[3], pw[3], rel[3];
+        loc[ai] = si * hi[ai];
+        loc[b1] = cu[q] * hi[b1];
+        loc[b2] = cv[q] * hi[b2];
+        m3_vec(Ri, loc, pw);
+        for (int j = 0; j < 3; j++) rel[j] = pw[j] + cen[inc][j] - cf[j];
+        P[q][0] = v3_dot(rel, t1);
+        P[q][1] = v3_dot(rel, t2);
+        P[q][2] = v3_dot(rel, nref);
+    }
+    double uvd[24][3];
+    int ok[24];
+    int m = 0;
+    /* 1. incident vertices inside the reference rectangle */
+    for (int q = 0; q < 4; q++, m++) {
+        ok[m] = fabs(P[q][0]) <= hu && fabs(P[q][1]) <= hv;
+        memcpy(uvd[m], P[q], sizeof P[q]);
+    }
+    /* 2. reference corners inside the incident quadrilateral (same side of
+     *    its four edges), depth on the incident face's plane */
+    double e1[3] = {P[1][0] - P[0][0], P[1][1] - P[0][1], P[1][2] - P[0][2]};
+    double e3[3] = {P[3][0] - P[0][0], P[3][1] - P[0][1], P[3][2] - P[0][2]};
+    double pn[3];
+    v3_cross(e1, e3, pn);
+    for (int q = 0; q < 4; q++, m++) {
+        double u = cu[q] * hu, v = cv[q] * hv;
+        int pos = 1, neg = 1;
+        for (int e = 0; e < 4; e++) {
+            const double *a = P[e], *b = P[(e + 1) % 4];
+            double cr = (b[0] - a[0]) * (v - a[1]) - (b[1] - a[1]) * (u - a[0]);
+            pos = pos && cr >= 0.0;
+            neg = neg && cr <= 0.0;
+        }
+        ok[m] = (pos || neg) && pn[2] != 0.0;
+        uvd[m][0] = u;
+        uvd[m][1] = v;
+        uvd[m][2] = pn[2] != 0.0 ? P[0][2] - (pn[0] * (u - P[0][0]) + pn[1] * (v - P[0][1])) / pn[2] : 0.0;
+    }
+    /* 3. incident edges crossing the rectangle's edges */
+    for (int e = 0; e < 4; e++) {
+        const double *a = P[e], *b = P[(e + 1) % 4];
+        for (int s = 0; s < 4; s++, m++) {
+            int on_u = s < 2; /* edges u = +-hu (s = 0, 1), v = +-hv (s = 2, 3) */
+            double lim = (s & 1) ? -(on_u ? hu : hv) : (on_u ? hu : hv);
+            double ca = on_u ? a[0] : a[1], cb = on_u ? b[0] : b[1];
+            double den = cb - ca;
+            double t = den != 0.0 ? (lim - ca) / den : -1.0;
+            double u = a[0] + t * (b[0] - a[0]), v = a[1] + t * (b[1] - a[1]);
+            ok[m] = t > 0.0 && t < 1.0 && (on_u ? fabs(v) <= hv : fabs(u) <= hu);
+            uvd[m][0] = on_u ? lim : u;
+            uvd[m][1] = on_u ? v : lim;
+            uvd[m][2] = a[2] + t * (b[2] - a[2]);
+        }
+    }
+    int n = 0;
+    for (int q = 0; q < m; q++) {
+        if (!ok[q]) continue;
+        ocand *c = &cand[n++];
+        double pref[3], pinc[3];
+        for (int j = 0; j < 3; j++) {
+            pref[j] = cf[j] + uvd[q][0] * t1[j] + uvd[q][1] * t2[j];
+            pinc[j] = pref[j] + nref[j] * uvd[q][2];
+        }
+        c->dist = uvd[q][2];
+        if (ref == 1) { /* the cube is the reference: n (cube -> box) = nref */
+            memcpy(c->pA, pinc, sizeof pinc);
+            memcpy(c->pB, pref, sizeof pref);
+            memcpy(c->n, nref, sizeof nref);
+        } else {
+            memcpy(c->pA, pref, sizeof pref);
+            memcpy(c->pB, pinc, sizeof pinc);
+            for (int j = 0; j < 3; j++) c->n[j] = -nref[j];
+        }
+    }
+    return n;
+}
+
+/* robot box vs the cylinder (object frame of the cylinder: R, centre x) */
+static int box_cyl_cands(const po_config *cfg, const double xc[3], const double xR[9], const double xh[3],
+                         const double yc[3], const double yR[9], ocand *cand) {
+    const double r = cfg->object_half[0], hh = cfg->object_half[2];
+    int n = 0;
+    /* box centre and axes in the cylinder frame */
+    double rel[3] = {xc[0] - yc[0], xc[1] - yc[1], xc[2] - yc[2]}, bc[3], bR[9];
+    m3_tvec(yR, rel, bc);
+    for (int a = 0; a < 3; a++) {
+        double col[3] = {xR[a], xR[3 + a], xR[6 + a]}, lc[3];
+        m3_tvec(yR, col, lc);
+        bR[a] = lc[0]; bR[3 + a] = lc[1]; bR[6 + a] = lc[2];
+    }
+    /* local candidate -> world */
+    double lA[3], lB[3], ln[3], ldist;
+#define OL_PUSH()                                                   \
+    do {                                                            \
+        ocand *c_ = &cand[n++];                                     \
+        m3_vec(yR, lA, c_->pA);                                     \
+        m3_vec(yR, lB, c_->pB);                                     \
+        m3_vec(yR, ln, c_->n);                                      \
+        for (int j_ = 0; j_ < 3; j_++) {                            \
+            c_->pA[j_] += yc[j_];                                   \
+            c_->pB[j_] += yc[j_];                                   \
+        }                                                           \
+        c_->dist = ldist;                                           \
+    } while (0)
+    /* 1. box vertices vs the solid */
+    for (int v = 0; v < 8; v++) {
+        double loc[3] = {(v & 1) ? xh[0] : -xh[0], (v & 2) ? xh[1] : -xh[1], (v & 4) ? xh[2] : -xh[2]}, w[3];
+        m3_vec(bR, loc, w);
+        for (int j = 0; j < 3; j++) lA[j] = bc[j] + w[j];
+        ldist = object_closest(cfg, lA, lB, ln);
+        OL_PUSH();
+    }
+    /* 2. side faces of the box vs the generator line facing them */
+    for (int f = 0; f < 6; f++) {
+        int ax = f >> 1;
+        double sg = (f & 1) ? -1.0 : 1.0;
+        double nf[3] = {sg * bR[ax], sg * bR[3 + ax], sg * bR[6 + ax]};
+        double nxy = sqrt(nf[0] * nf[0] + nf[1] * nf[1]);
+        if (!(fabs(nf[2]) < 0.5)) continue; /* caps are covered by 1 and 3 */
+        int a1 = (ax + 1) % 3, a2 = (ax + 2) % 3;
+        double fc[3], t1[3] = {bR[a1], bR[3 + a1], bR[6 + a1]}, t2[3] = {bR[a2], bR[3 + a2], bR[6 + a2]};
+        for (int j = 0; j < 3; j++) fc[j] = bc[j] + nf[j] * xh[ax];
+        /* generator s(z) = (-r nf_xy / |nf_xy|, z): u, v, depth and the axis
+         * side test are affine in z; clip z to where all four in-face
+         * constraints, the axis test and |z| <= hh hold */
+        double s0[3] = {-r * nf[0] / nxy, -r * nf[1] / nxy, 0.0}, d0[3];
+        for (int j = 0; j < 3; j++) d0[j] = s0[j] - fc[j];
+        double lo = -hh, hi = hh;
+        /* each constraint: k0 + k1 z <= lim */
+        double K[5][3] = {
+            {v3_dot(d0, t1), t1[2], xh[a1]},  {-v3_dot(d0, t1), -t1[2], xh[a1]},
+            {v3_dot(d0, t2), t2[2], xh[a2]},  {-v3_dot(d0, t2), -t2[2], xh[a2]},
+            /* the axis point (0, 0, z) outside the face plane: nf . ((0,0,z) - fc) >= 0 */
+            {v3_dot(nf, fc), -nf[2], 0.0},
+        };
+        for (int k = 0; k < 5; k++) {
+            double k0 = K[k][0], k1 = K[k][1], lim = K[k][2];
+            if (k1 > 1e-12) { double z = (lim - k0) / k1; hi = z < hi ? z : hi; }
+            else if (k1 < -1e-12) { double z = (lim - k0) / k1; lo = z > lo ? z : lo; }
+            else if (k0 > lim) { lo = 1.0; hi = -1.0; }
+        }
+        if (!(lo <= hi)) continue;
+        for (int e = 0; e < 2; e++) {
+            double z = e ? hi : lo;
+            lB[0] = s0[0]; lB[1] = s0[1]; lB[2] = z;
+            double dd[3] = {lB[0] - fc[0], lB[1] - fc[1], lB[2] - fc[2]};
+            ldist = v3_dot(nf, dd);
+            for (int j = 0; j < 3; j++) {
+                lA[j] = lB[j] - nf[j] * ldist;
+                ln[j] = -nf[j];
+            }
+            OL_PUSH();
+        }
+    }
+    /* 3. rim points vs the box */
+    double pts[2 * PM_CYL_RIM_POINTS][3];
+    int np = object_support_points(cfg, pts);
+    for (int p = 0; p < np; p++) {
+        double dl[3] = {pts[p][0] - bc[0], pts[p][1] - bc[1], pts[p][2] - bc[2]}, lp[3], cl[3], dif[3];
+        m3_tvec(bR, dl, lp); /* rim point in the box frame */
+        for (int j = 0; j < 3; j++) {
+            cl[j] = lp[j] < -xh[j] ? -xh[j] : (lp[j] > xh[j] ? xh[j] : lp[j]);
+            dif[j] = lp[j] - cl[j];
+        }
+        double dn = v3_norm(dif), nb[3];
+        if (dn > 1e-9) {
+            for (int j = 0; j < 3; j++) nb[j] = dif[j] / dn;
+            ldist = dn;
+        } else {
+            int ax = 0;
+            double bst = xh[0] - fabs(lp[0]);
+            for (int j = 1; j < 3; j++)
+                if (xh[j] - fabs(lp[j]) < bst) { bst = xh[j] - fabs(lp[j]); ax = j; }
+            nb[0] = nb[1] = nb[2] = 0.0;
+            nb[ax] = lp[ax] >= 0.0 ? 1.0 : -1.0;
+            cl[ax] = nb[ax] * xh[ax];
+            ldist = -bst;
+        }
+        double w[3], wn[3];
+        m3_vec(bR, cl, w);
+        m3_vec(bR, nb, wn); /* box outward normal at the point, cylinder frame */
+        for (int j = 0; j < 3; j++) {
+            lA[j] = bc[j] + w[j];
+            lB[j] = pts[p][j];
+            ln[j] = -wn[j];
+        }
+        OL_PUSH();
+    }
+#undef OL_PUSH
+    return n;
+}
+
+/* robot box vs the ground (table top or plane) */
+static int box_ground_cands(const po_config *cfg, const double xc[3], const double xR[9], const double xh[3],
+                            ocand *cand) {
+    int n = 0;
+    for (int v = 0; v < 8; v++) {
+        double loc[3] = {(v & 1) ? xh[0] : -xh[0], (v & 2) ? xh[1] : -xh[1], (v & 4) ? xh[2] : -xh[2]}, w[3], top;
+        m3_vec(xR, loc, w);
+        double p[3] = {xc[0] + w[0], xc[1] + w[1], xc[2] + w[2]};
+        if (!ground_top(cfg, p[0], p[1], &top)) continue;
+        ocand *c = &cand[n++];
+        memcpy(c->pA, p, sizeof p);
+        c->pB[0] = p[0]; c->pB[1] = p[1]; c->pB[2] = top;
+        c->n[0] = 0.0; c->n[1] = 0.0; c->n[2] = 1.0;
+        c->dist = p[2] - top;
+    }
+    return n;
+}
+
 /* Contact generation (replaces Bullet's broadphase + box-box / convex
  * narrowphase with the proxies of panda_model.h), fixed order and caps:
  *   1. per object: support points (box vertices / cylinder rim points) vs
  *      ground (table top or plane): the first PM_MAX_GROUND_CONTACTS within
  *      the margin, in candidate order
  *   2. object-object (Stack): box_box_contacts
- *   3. gripper spheres vs object 1, vs object 2 (closest point on the solid)
- *   4. gripper spheres vs ground
- *   3+4 share PM_MAX_ROBOT_CONTACTS slots, filled in that order.
+ *   3. per object: the gripper boxes (fingers, palm; PM_BOX_CONTACTS each),
+ *      then the wrist sphere (closest point on the solid)
+ *   4. the gripper boxes, then the wrist sphere, vs ground
+ *   3+4 share PM_MAX_ROBOT_CONTACTS slots, filled in that order.  Cache ids
+ *   (warm start): 1 + (proxy * 3 + target) * 2 + point, proxy 0-2 the boxes,
+ *   3 the wrist, target 0/1 the objects, 2 the ground.
  * Friction coefficients are products of the two bodies' lateral frictions
- * (objects: object_friction, ground/table: 0.5, gripper spheres: their own). */
+ * (objects: object_friction, ground/table: 0.5, gripper proxies: their own). */
 static int gen_contacts(const po_config *cfg, const po_env *env, const okin *k, const oobj *ob, ocontact *out) {
     int nc = 0;
-    double sc[PM_NUM_SPHERES][3];
-    if (cfg->has_robot)
-        for (int s = 0; s < PM_NUM_SPHERES; s++) {
-            double t[3];
-            m3_vec(k->R[SPH[s].link], SPH[s].c, t);
-            for (int d = 0; d < 3; d++) sc[s][d] = k->o[SPH[s].link][d] + t[d];
-        }
+    /* the wrist sphere (link 7) */
+    int wlink = 0;
+    double wc[3] = {0, 0, 0}, wr = 0.0, wmu = 0.0;
+    if (cfg->has_robot) {
+#define OL_WRIST(link_, x, y, z, rad, mu_)                                  \
+    {                                                                       \
+        double c_[3] = {x, y, z}, t_[3];                                    \
+        wlink = link_;                                                      \
+        m3_vec(k->R[link_], c_, t_);                                        \
+        for (int d_ = 0; d_ < 3; d_++) wc[d_] = k->o[link_][d_] + t_[d_];   \
+        wr = rad;                                                           \
+        wmu = mu_;                                                          \
+    }
+        PM_WRIST_SPHERE(OL_WRIST)
+#undef OL_WRIST
+    }
     double pts[2 * PM_CYL_RIM_POINTS][3];
     int npts = object_support_points(cfg, pts);
     for (int i = 0; i < cfg->n_objects; i++) {
@@ -858,47 +1201,77 @@ static int gen_contacts(const po_config *cfg, const po_env *env, const okin *k, 
     if (cfg->n_objects == 2) box_box_contacts(cfg, env, ob, out, &nc);
     int nr = 0;
     if (cfg->has_robot) {
-        for (int i = 0; i < cfg->n_objects; i++)
-            for (int s = 0; s < PM_NUM_SPHERES && nr < PM_MAX_ROBOT_CONTACTS; s++) {
-                const po_body *b = &env->obj[i];
-                double rel[3] = {sc[s][0] - b->pos[0], sc[s][1] - b->pos[1], sc[s][2] - b->pos[2]}, loc[3];
-                m3_tvec(ob[i].R, rel, loc);
-                double cl[3], nl[3];
-                double dist = object_closest(cfg, loc, cl, nl) - SPH[s].r;
+        /* target 0, 1: the objects; 2: the ground */
+        for (int tgt = 0; tgt < 3; tgt++) {
+            int ground = tgt == 2;
+            if (!ground && tgt >= cfg->n_objects) continue;
+            for (int bx = 0; bx < PM_NUM_BOXES && nr < PM_MAX_ROBOT_CONTACTS; bx++) {
+                double xc[3], xR[9];
+                robot_box(k, bx, xc, xR);
+                ocand cand[40], sel[2];
+                int m;
+                if (ground) m = box_ground_cands(cfg, xc, xR, BOXES[bx].h, cand);
+                else if (cfg->object_shape == PO_SHAPE_CYLINDER)
+                    m = box_cyl_cands(cfg, xc, xR, BOXES[bx].h, env->obj[tgt].pos, ob[tgt].R, cand);
+                else
+                    m = box_cube_cands(xc, xR, BOXES[bx].h, env->obj[tgt].pos, ob[tgt].R, cfg->object_half, cand);
+                int ns = pick_contacts(cand, m, xc, xR, longest_axis(BOXES[bx].h), sel);
+                for (int q = 0; q < ns && nr < PM_MAX_ROBOT_CONTACTS; q++) {
+                    ocontact *c = &out[nc++];
+                    nr++;
+                    c->bodyA = BOXES[bx].link;
+                    c->bodyB = ground ? BODY_STATIC : BODY_OBJ(tgt);
+                    memcpy(c->pA, sel[q].pA, sizeof c->pA);
+                    memcpy(c->pB, sel[q].pB, sizeof c->pB);
+                    memcpy(c->n, sel[q].n, sizeof c->n);
+                    c->dist = sel[q].dist;
+                    c->mu = BOXES[bx].mu * (ground ? PM_DEFAULT_FRICTION : cfg->object_friction);
+                    c->group = CG_ROBOT;
+                    c->id = 1 + (bx * 3 + tgt) * 2 + q;
+                }
+            }
+            if (nr >= PM_MAX_ROBOT_CONTACTS) continue;
+            /* the wrist sphere */
+            if (ground) {
+                double top;
+                if (!ground_top(cfg, wc[0], wc[1], &top)) continue;
+                double dist = wc[2] - wr - top;
                 if (dist < PM_CONTACT_MARGIN_SPHERE) {
                     ocontact *c = &out[nc++];
                     nr++;
-                    c->bodyA = SPH[s].link;
-                    c->bodyB = BODY_OBJ(i);
-                    m3_vec(ob[i].R, nl, c->n);
+                    c->bodyA = wlink;
+                    c->bodyB = BODY_STATIC;
+                    c->n[0] = 0; c->n[1] = 0; c->n[2] = 1;
+                    c->pA[0] = wc[0]; c->pA[1] = wc[1]; c->pA[2] = wc[2] - wr;
+                    c->pB[0] = wc[0]; c->pB[1] = wc[1]; c->pB[2] = top;
+                    c->dist = dist;
+                    c->mu = wmu * PM_DEFAULT_FRICTION;
+                    c->group = CG_ROBOT;
+                    c->id = 1 + (PM_NUM_BOXES * 3 + tgt) * 2;
+                }
+            } else {
+                const po_body *b = &env->obj[tgt];
+                double rel[3] = {wc[0] - b->pos[0], wc[1] - b->pos[1], wc[2] - b->pos[2]}, loc[3];
+                m3_tvec(ob[tgt].R, rel, loc);
+                double cl[3], nl[3];
+                double dist = object_closest(cfg, loc, cl, nl) - wr;
+                if (dist < PM_CONTACT_MARGIN_SPHERE) {
+                    ocontact *c = &out[nc++];
+                    nr++;
+                    c->bodyA = wlink;
+                    c->bodyB = BODY_OBJ(tgt);
+                    m3_vec(ob[tgt].R, nl, c->n);
                     double pw[3];
-                    m3_vec(ob[i].R, cl, pw);
+                    m3_vec(ob[tgt].R, cl, pw);
                     for (int d = 0; d < 3; d++) {
                         c->pB[d] = b->pos[d] + pw[d];
-                        c->pA[d] = sc[s][d] - c->n[d] * SPH[s].r;
+                        c->pA[d] = wc[d] - c->n[d] * wr;
                     }
                     c->dist = dist;
-                    c->mu = SPH[s].mu * cfg->object_friction;
+                    c->mu = wmu * cfg->object_friction;
                     c->group = CG_ROBOT;
-                    c->id = 1 + s + 8 * i;
+                    c->id = 1 + (PM_NUM_BOXES * 3 + tgt) * 2;
                 }
-            }
-        for (int s = 0; s < PM_NUM_SPHERES && nr < PM_MAX_ROBOT_CONTACTS; s++) {
-            double top;
-            if (!ground_top(cfg, sc[s][0], sc[s][1], &top)) continue;
-            double dist = sc[s][2] - SPH[s].r - top;
-            if (dist < PM_CONTACT_MARGIN_SPHERE) {
-                ocontact *c = &out[nc++];
-                nr++;
-                c->bodyA = SPH[s].link;
-                c->bodyB = BODY_STATIC;
-                c->n[0] = 0; c->n[1] = 0; c->n[2] = 1;
-                c->pA[0] = sc[s][0]; c->pA[1] = sc[s][1]; c->pA[2] = sc[s][2] - SPH[s].r;
-                c->pB[0] = sc[s][0]; c->pB[1] = sc[s][1]; c->pB[2] = top;
-                c->dist = dist;
-                c->mu = SPH[s].mu * PM_DEFAULT_FRICTION;
-                c->group = CG_ROBOT;
-                c->id = 1 + s + 8 * 2;
             }
         }
     }

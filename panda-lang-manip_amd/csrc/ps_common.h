@@ -21,8 +21,9 @@
 #define PS_NUM_PHASES 8
 #define PS_NUM_PROF_SLOTS 20  // phases + PGS counters (lane iterations, wave iterations, substeps, robot-contact slots run,
                               // the wave's open row gates: pair slots, ground slots, robot slots, joint limits;
-                              // 16-18: sub-phases of rows+contacts -- joint rows, object ground/pair contacts,
-                              // gripper contact candidates -- the rest of it, the gripper rows, stays in 3)
+                              // 16-18: sub-phases of rows+contacts -- 16 joint rows, 17 gripper contact
+                              // candidates, 18 object ground/pair contacts -- the rest of it, the gripper
+                              // rows, stays in 3)
 #ifdef PS_PROFILE_PHASES
 struct PhaseTimer {
     uint64_t last, acc[PS_NUM_PROF_SLOTS];
@@ -214,6 +215,27 @@ struct SphereDef {
 PS_HD constexpr SphereDef sphere_def(int s) {
     const SphereDef t[PM_NUM_SPHERES] = {PM_SPHERE_TABLE(PS_SPHDEF)};
     return t[s];
+}
+
+// gripper collision boxes (PM_BOX_TABLE) and the wrist sphere (PM_WRIST_SPHERE)
+struct BoxDef {
+    int link;
+    double c[3], h[3], mu;
+};
+#define PS_BOXDEF(link, cx, cy, cz, hx, hy, hz, mu) BoxDef{link, {cx, cy, cz}, {hx, hy, hz}, mu},
+PS_HD constexpr BoxDef box_def(int b) {
+    const BoxDef t[PM_NUM_BOXES] = {PM_BOX_TABLE(PS_BOXDEF)};
+    return t[b];
+}
+PS_HD constexpr SphereDef wrist_def() {
+    const SphereDef t[1] = {PM_WRIST_SPHERE(PS_SPHDEF)};
+    return t[0];
+}
+// the box's longest axis (the order of its two contact points)
+PS_HD constexpr int box_long_axis(int b) {
+    return box_def(b).h[2] >= box_def(b).h[1] && box_def(b).h[2] >= box_def(b).h[0]
+               ? 2
+               : (box_def(b).h[1] >= box_def(b).h[0] ? 1 : 0);
 }
 
 PS_HD constexpr double joint_force(int d) {

@@ -661,10 +661,293 @@ PS_D float jrow_dot(const float J[9], const float v[9]) {
 }
 
 // Geometry that outlives the kinematics: DoF axes/origins (gripper-contact
-// Jacobians) and world sphere centres.
+// Jacobians), the hand's rotation (every gripper box's: the finger frames are
+// the hand's, translated), the world box centres and the wrist sphere centre.
 struct Geo {
-    V3 ax[9], org[7], spw[PM_NUM_SPHERES];
+    V3 ax[9], org[7], bc[PM_NUM_BOXES], wc;
+    M3 hR;
 };
+
+// ------------------------------------------------- gripper collision boxes
+// The oracle's gen_contacts restated in fp32 (oracle/panda_oracle.c
+// box_cube_cands / box_cyl_cands / box_ground_cands / pick_contacts, DESIGN.md
+// §5): each (box, target) pair offers at most PM_BOX_CONTACTS points, picked
+// from a fixed candidate stream -- the deepest within the margin, then the one
+// farthest from it -- and ordered along the box's longest axis.  The stream is
+// visited twice (once per pick) instead of being stored: its expensive part
+// (separating axis, reference and incident faces) is computed once, the
+// candidates themselves are a few FMAs each.
+struct RCand {
+    V3 pA, pB, n;  // robot point, object/ground point, normal from B to A
+    float dist;
+};
+PS_D float comp(V3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+PS_D V3 colsel(const M3 &R, int c) { return c == 0 ? col(R, 0) : (c == 1 ? col(R, 1) : col(R, 2)); }
+
+template <class Visit>
+PS_D int pick_two(Visit &&visit, V3 org, V3 axis, RCand &c0, RCand &c1) {
+    const float margin = (float)PM_CONTACT_MARGIN_ROBOT;
+    bool has0 = false, has1 = false;
+    c0 = c1 = RCand{mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 1), 1.0f};
+    visit([&](bool ok, const RCand &c) {
+        if (ok && c.dist < margin && (!has0 || c.dist < c0.dist)) {
+            c0 = c;
+            has0 = true;
+        }
+    });
+    float best = 1e-8f;  // (0.1 mm)^2
+    visit([&](bool ok, const RCand &c) {
+        const V3 d = c.pA - c0.pA;
+        const float d2 = dot(d, d);
+        if (has0 && ok && c.dist < margin && d2 > best) {
+            best = d2;
+            c1 = c;
+            has1 = true;
+        }
+    });
+    if (has1 && dot(c1.pA - org, axis) < dot(c0.pA - org, axis)) {
+        const RCand t = c0;
+        c0 = c1;
+        c1 = t;
+    }
+    return has0 ? (has1 ? 2 : 1) : 0;
+}
+
+// robot box (centre xc, rotation xR, half extents xh) vs a cube (yc, yR, yh)
+struct BoxCube {
+    bool sep;
+    V3 nref, t1, t2, cf;
+    float hu, hv;
+    bool robot_ref;
+    float P[4][3];  // incident face vertices (u, v, depth below the reference face)
+    PS_D BoxCube(V3 xc, const M3 &xR, V3 xh, V3 yc, const M3 &yR, V3 yh) {
+        const V3 d = yc - xc;
+        float best = 1e30f;
+        int ref = 0, axn = 0;
+        sep = false;
+        nref = mk(0, 0, 0);
+#pragma unroll
+        for (int b = 0; b < 2; b++)
+#pragma unroll
+            for (int ax = 0; ax < 3; ax++) {
+                const V3 L = col(b == 0 ? xR : yR, ax);
+                const float ra = xh.x * fabsf(dot(col(xR, 0), L)) + xh.y * fabsf(dot(col(xR, 1), L)) +
+                                 xh.z * fabsf(dot(col(xR, 2), L));
+                const float rb = yh.x * fabsf(dot(col(yR, 0), L)) + yh.y * fabsf(dot(col(yR, 1), L)) +
+                                 yh.z * fabsf(dot(col(yR, 2), L));
+                const float c = dot(d, L);
+                const float pen = ra + rb - fabsf(c);
+                sep = sep || pen < -(float)PM_CONTACT_MARGIN_ROBOT;
+                if (pen < best - (float)PM_PAIR_AXIS_TOL) {
+                    best = pen;
+                    ref = b;
+                    axn = ax;
+                    nref = L * ((b == 0 ? c : -c) >= 0.0f ? 1.0f : -1.0f);
+                }
+            }
+        robot_ref = ref == 0;
+        const int a1 = axn == 2 ? 0 : axn + 1, a2 = axn == 0 ? 2 : axn - 1;
+        const V3 hr = robot_ref ? xh : yh, hi = robot_ref ? yh : xh;
+        const V3 cr = robot_ref ? xc : yc, ci = robot_ref ? yc : xc;
+        M3 Rr, Ri;
+#pragma unroll
+        for (int k = 0; k < 9; k++) {
+            Rr.m[k] = robot_ref ? xR.m[k] : yR.m[k];
+            Ri.m[k] = robot_ref ? yR.m[k] : xR.m[k];
+        }
+        t1 = colsel(Rr, a1);
+        t2 = colsel(Rr, a2);
+        cf = cr + nref * comp(hr, axn);
+        hu = comp(hr, a1);
+        hv = comp(hr, a2);
+        // incident face: the incident box's axis most anti-parallel to nref
+        int ai = 0;
+        float mostneg = 2.0f, si = 1.0f;
+#pragma unroll
+        for (int ax = 0; ax < 3; ax++) {
+            const float dn = dot(col(Ri, ax), nref);
+            if (-fabsf(dn) < mostneg) {
+                mostneg = -fabsf(dn);
+                ai = ax;
+                si = dn > 0.0f ? -1.0f : 1.0f;
+            }
+        }
+        const int b1 = ai == 2 ? 0 : ai + 1, b2 = ai == 0 ? 2 : ai - 1;
+        const V3 ea = colsel(Ri, ai) * (si * comp(hi, ai)), eb = colsel(Ri, b1) * comp(hi, b1),
+                 ec = colsel(Ri, b2) * comp(hi, b2);
+        const V3 base = ci - cf;
+        constexpr float cu[4] = {-1, 1, 1, -1}, cv[4] = {-1, -1, 1, 1};
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const V3 rel = base + ea + eb * cu[q] + ec * cv[q];
+            P[q][0] = dot(rel, t1);
+            P[q][1] = dot(rel, t2);
+            P[q][2] = dot(rel, nref);
+        }
+    }
+    template <class F>
+    PS_D void visit(F &&f) const {
+        auto emit = [&](bool ok, float u, float v, float depth) {
+            const V3 pref = cf + t1 * u + t2 * v, pinc = pref + nref * depth;
+            f(ok && !sep, RCand{robot_ref ? pref : pinc, robot_ref ? pinc : pref, robot_ref ? -nref : nref, depth});
+        };
+        constexpr float cu[4] = {-1, 1, 1, -1}, cv[4] = {-1, -1, 1, 1};
+        // 1. incident vertices inside the reference rectangle
+#pragma unroll
+        for (int q = 0; q < 4; q++) emit(fabsf(P[q][0]) <= hu && fabsf(P[q][1]) <= hv, P[q][0], P[q][1], P[q][2]);
+        // 2. reference corners inside the incident quadrilateral, depth on its plane
+        const float e1u = P[1][0] - P[0][0], e1v = P[1][1] - P[0][1], e1d = P[1][2] - P[0][2];
+        const float e3u = P[3][0] - P[0][0], e3v = P[3][1] - P[0][1], e3d = P[3][2] - P[0][2];
+        const float pnu = e1v * e3d - e1d * e3v, pnv = e1d * e3u - e1u * e3d, pnd = e1u * e3v - e1v * e3u;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const float u = cu[q] * hu, v = cv[q] * hv;
+            bool pos = true, neg = true;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const int e2 = (e + 1) & 3;
+                const float cr = (P[e2][0] - P[e][0]) * (v - P[e][1]) - (P[e2][1] - P[e][1]) * (u - P[e][0]);
+                pos = pos && cr >= 0.0f;
+                neg = neg && cr <= 0.0f;
+            }
+            const bool okp = pnd != 0.0f;
+            const float depth = okp ? P[0][2] - (pnu * (u - P[0][0]) + pnv * (v - P[0][1])) / pnd : 0.0f;
+            emit((pos || neg) && okp, u, v, depth);
+        }
+        // 3. incident edges crossing the rectangle's edges (u = +-hu, v = +-hv)
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int e2 = (e + 1) & 3;
+#pragma unroll
+            for (int s = 0; s < 4; s++) {
+                const bool on_u = s < 2;
+                const float lim = (s & 1) ? -(on_u ? hu : hv) : (on_u ? hu : hv);
+                const float ca = on_u ? P[e][0] : P[e][1], cb = on_u ? P[e2][0] : P[e2][1];
+                const float den = cb - ca;
+                const float t = den != 0.0f ? (lim - ca) / den : -1.0f;
+                const float u = P[e][0] + t * (P[e2][0] - P[e][0]), v = P[e][1] + t * (P[e2][1] - P[e][1]);
+                const bool ok = t > 0.0f && t < 1.0f && (on_u ? fabsf(v) <= hv : fabsf(u) <= hu);
+                emit(ok, on_u ? lim : u, on_u ? v : lim, P[e][2] + t * (P[e2][2] - P[e][2]));
+            }
+        }
+    }
+};
+
+// robot box vs the cylinder (Slide), in the cylinder's frame
+struct BoxCyl {
+    V3 bc, yc;
+    M3 bR, yR;
+    V3 xh;
+    float r, hh;
+    PS_D BoxCyl(const Scene &sc, V3 xc, const M3 &xR, V3 xh_, V3 yc_, const M3 &yR_) : yc(yc_), yR(yR_), xh(xh_) {
+        r = sc.half.x;
+        hh = sc.half.z;
+        bc = tmul(yR, xc - yc);
+#pragma unroll
+        for (int a = 0; a < 3; a++) {
+            const V3 lc = tmul(yR, col(xR, a));
+            bR.m[a] = lc.x;
+            bR.m[3 + a] = lc.y;
+            bR.m[6 + a] = lc.z;
+        }
+    }
+    template <class F>
+    PS_D void visit(const Scene &sc, F &&f) const {
+        auto emit = [&](bool ok, V3 lA, V3 lB, V3 ln, float dist) {
+            f(ok, RCand{yc + mul(yR, lA), yc + mul(yR, lB), mul(yR, ln), dist});
+        };
+        // 1. box vertices vs the solid (the loops stay rolled: unrolled, the
+        // two visits of the 36 candidates spilled ~300 VGPRs in Slide's kernels)
+#pragma unroll 1
+        for (int v = 0; v < 8; v++) {
+            const V3 lA = bc + mul(bR, mk((v & 1) ? xh.x : -xh.x, (v & 2) ? xh.y : -xh.y, (v & 4) ? xh.z : -xh.z));
+            V3 cl, nl;
+            const float dist = object_closest<SHAPE_CYL>(sc, lA, cl, nl);
+            emit(true, lA, cl, nl, dist);
+        }
+        // 2. side faces of the box vs the generator line facing them
+#pragma unroll 1
+        for (int fc = 0; fc < 6; fc++) {
+            const int ax = fc >> 1;
+            const float sg = (fc & 1) ? -1.0f : 1.0f;
+            const V3 nf = colsel(bR, ax) * sg;
+            const int a1 = ax == 2 ? 0 : ax + 1, a2 = ax == 0 ? 2 : ax - 1;
+            const V3 t1 = colsel(bR, a1), t2 = colsel(bR, a2);
+            const float h1 = comp(xh, a1), h2 = comp(xh, a2);
+            const V3 fcen = bc + nf * comp(xh, ax);
+            const bool side = fabsf(nf.z) < 0.5f;
+            const float nxy = sqrtf(nf.x * nf.x + nf.y * nf.y);
+            const float inv = side ? r / nxy : 0.0f;
+            const V3 s0 = mk(-nf.x * inv, -nf.y * inv, 0.0f), d0 = s0 - fcen;
+            float lo = -hh, hi = hh;
+            const float K[5][3] = {{dot(d0, t1), t1.z, h1},
+                                   {-dot(d0, t1), -t1.z, h1},
+                                   {dot(d0, t2), t2.z, h2},
+                                   {-dot(d0, t2), -t2.z, h2},
+                                   {dot(nf, fcen), -nf.z, 0.0f}};
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                const float k0 = K[k][0], k1 = K[k][1], lim = K[k][2];
+                const float z = (lim - k0) / k1;
+                if (k1 > 1e-12f) hi = fminf(z, hi);
+                else if (k1 < -1e-12f) lo = fmaxf(z, lo);
+                else if (k0 > lim) { lo = 1.0f; hi = -1.0f; }
+            }
+            const bool ok = side && lo <= hi;
+#pragma unroll
+            for (int e = 0; e < 2; e++) {
+                const V3 lB = mk(s0.x, s0.y, e ? hi : lo);
+                const float dist = dot(nf, lB - fcen);
+                emit(ok, lB - nf * dist, lB, -nf, dist);
+            }
+        }
+        // 3. rim points vs the box (support_point<SHAPE_CYL, V>'s order and values)
+        constexpr int order[PM_CYL_RIM_POINTS] = PM_CYL_RIM_ORDER;
+        constexpr float c45 = 0.70710678118654752f;
+#pragma unroll 1
+        for (int V = 0; V < num_support<SHAPE_CYL>(); V++) {
+            int j = 0;
+#pragma unroll
+            for (int k = 0; k < PM_CYL_RIM_POINTS; k++) j = (V % PM_CYL_RIM_POINTS) == k ? order[k] : j;
+            const float cs = j == 0 ? 1.0f : j == 1 || j == 7 ? c45 : j == 2 || j == 6 ? 0.0f : j == 4 ? -1.0f : -c45;
+            const float sn = j == 2 ? 1.0f : j == 1 || j == 3 ? c45 : j == 0 || j == 4 ? 0.0f : j == 6 ? -1.0f : -c45;
+            const V3 p = mk(sc.half.x * cs, sc.half.x * sn, V >= PM_CYL_RIM_POINTS ? sc.half.z : -sc.half.z);
+            const V3 lp = tmul(bR, p - bc);
+            V3 cl = mk(fminf(fmaxf(lp.x, -xh.x), xh.x), fminf(fmaxf(lp.y, -xh.y), xh.y), fminf(fmaxf(lp.z, -xh.z), xh.z));
+            const V3 dif = lp - cl;
+            const float dn = norm(dif);
+            V3 nb;
+            float dist;
+            if (dn > 1e-9f) {
+                nb = dif * (1.0f / dn);
+                dist = dn;
+            } else {
+                const float bx = xh.x - fabsf(lp.x), by = xh.y - fabsf(lp.y), bz = xh.z - fabsf(lp.z);
+                int ax = 0;
+                float bst = bx;
+                if (by < bst) { bst = by; ax = 1; }
+                if (bz < bst) { bst = bz; ax = 2; }
+                const float s = comp(lp, ax) >= 0.0f ? 1.0f : -1.0f;
+                nb = ax == 0 ? mk(s, 0, 0) : (ax == 1 ? mk(0, s, 0) : mk(0, 0, s));
+                cl = ax == 0 ? mk(s * xh.x, cl.y, cl.z) : (ax == 1 ? mk(cl.x, s * xh.y, cl.z) : mk(cl.x, cl.y, s * xh.z));
+                dist = -bst;
+            }
+            emit(true, bc + mul(bR, cl), p, -mul(bR, nb), dist);
+        }
+    }
+};
+
+// robot box vs the ground (table top or plane)
+template <class F>
+PS_D void box_ground_visit(const Scene &sc, V3 xc, const M3 &xR, V3 xh, F &&f) {
+#pragma unroll
+    for (int v = 0; v < 8; v++) {
+        const V3 p = xc + mul(xR, mk((v & 1) ? xh.x : -xh.x, (v & 2) ? xh.y : -xh.y, (v & 4) ? xh.z : -xh.z));
+        float top = 0.0f;
+        const bool ok = ground_top(sc, p.x, p.y, top);
+        f(ok, RCand{p, mk(p.x, p.y, top), mk(0, 0, 1), p.z - top});
+    }
+}
 
 // row rhs of a contact normal (btSequentialImpulseConstraintSolver setup:
 // speculative margin when separated, ERP/split-impulse when penetrating)
@@ -1117,6 +1400,94 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
     }
 }
 
+// Gripper contact candidates (oracle gen_contacts 3-4): per object, then the
+// ground, the gripper boxes (PM_BOX_CONTACTS points each) and then the wrist
+// sphere; the first NR fill the slots.  Cache ids 1 + (proxy * 3 + target) * 2
+// + point.  Each slot's record (RobotCand, 14 floats) goes to LDS at the end of
+// the M^-1 J^T area, which the row setup overwrites only after it has read the
+// slot (slot s's rows are written to floats [27 s, 27 s + 27), its record sits
+// at [52 + 14 s, 66 + 14 s)).  Returns the number of slots used.
+struct RobotCand {
+    V3 pA, pB, n;
+    float dist, mu;
+    int link;
+    int obj;  // -1: ground
+    int id;   // cache id: 1 + (proxy * 3 + target) * 2 + point (target 2: the ground)
+    static constexpr int FLOATS = 14, OFFSET = NR * 27 - NR * 14;
+    PS_D void store(const MJStore &L, int s) const {
+        const float v[FLOATS] = {pA.x, pA.y, pA.z, pB.x, pB.y, pB.z, n.x, n.y, n.z, dist, mu,
+                                 (float)link, (float)obj, (float)id};
+#pragma unroll
+        for (int k = 0; k < FLOATS; k++) L.base[(OFFSET + s * FLOATS + k) * L.stride] = v[k];
+    }
+    PS_D static RobotCand load(const MJStore &L, int s) {
+        float v[FLOATS];
+#pragma unroll
+        for (int k = 0; k < FLOATS; k++) v[k] = L.base[(OFFSET + s * FLOATS + k) * L.stride];
+        return RobotCand{mk(v[0], v[1], v[2]), mk(v[3], v[4], v[5]), mk(v[6], v[7], v[8]), v[9], v[10],
+                         (int)v[11], (int)v[12], (int)v[13]};
+    }
+};
+static_assert(RobotCand::OFFSET + NR * RobotCand::FLOATS <= NR * 27, "candidate records inside the M^-1 J^T area");
+
+template <int NOBJ, int SHAPE>
+PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const M3 *oR, const MJStore &lds) {
+    int nr = 0;
+    auto offer = [&](const RobotCand &c) {
+        c.store(lds, nr);
+        nr++;
+    };
+    constexpr SphereDef ws = wrist_def();
+    static_for<0, NOBJ + 1>([&](auto TT) {
+        constexpr int TGT = decltype(TT)::value == NOBJ ? 2 : decltype(TT)::value;
+        constexpr bool GROUND = TGT == 2;
+        static_for<0, PM_NUM_BOXES>([&](auto BB) {
+            constexpr int B = decltype(BB)::value;
+            constexpr BoxDef bx = box_def(B);
+            const V3 xh = mk((float)bx.h[0], (float)bx.h[1], (float)bx.h[2]);
+            const V3 xc = geo.bc[B];
+            RCand c0, c1;
+            int ns = 0;
+            const V3 axis = col(geo.hR, box_long_axis(B));
+            if constexpr (GROUND) {
+                ns = pick_two([&](auto &&f) { box_ground_visit(sc, xc, geo.hR, xh, f); }, xc, axis, c0, c1);
+            } else if constexpr (SHAPE == SHAPE_CYL) {
+                const BoxCyl bcy(sc, xc, geo.hR, xh, bd[TGT].pos, oR[TGT]);
+                ns = pick_two([&](auto &&f) { bcy.visit(sc, f); }, xc, axis, c0, c1);
+            } else {
+                const BoxCube bcu(xc, geo.hR, xh, bd[TGT].pos, oR[TGT], sc.half);
+                ns = pick_two([&](auto &&f) { bcu.visit(f); }, xc, axis, c0, c1);
+            }
+            const float mu = (float)bx.mu * (GROUND ? (float)PM_DEFAULT_FRICTION : sc.fric);
+            const int obj = GROUND ? -1 : TGT;
+            if (nr < NR && ns >= 1) offer(RobotCand{c0.pA, c0.pB, c0.n, c0.dist, mu, bx.link, obj, 1 + (B * 3 + TGT) * 2});
+            if (nr < NR && ns >= 2) offer(RobotCand{c1.pA, c1.pB, c1.n, c1.dist, mu, bx.link, obj, 2 + (B * 3 + TGT) * 2});
+        });
+        constexpr int WID = 1 + (PM_NUM_BOXES * 3 + TGT) * 2;
+        if constexpr (GROUND) {
+            float top;
+            if (nr < NR && ground_top(sc, geo.wc.x, geo.wc.y, top)) {
+                const float dist = geo.wc.z - (float)ws.r - top;
+                if (dist < (float)PM_CONTACT_MARGIN_SPHERE) {
+                    const V3 pA = geo.wc - mk(0, 0, (float)ws.r);
+                    offer(RobotCand{pA, mk(pA.x, pA.y, top), mk(0, 0, 1), dist, (float)(ws.mu * PM_DEFAULT_FRICTION),
+                                    ws.link, -1, WID});
+                }
+            }
+        } else {
+            const V3 loc = tmul(oR[TGT], geo.wc - bd[TGT].pos);
+            V3 cl, nl;
+            const float dist = object_closest<SHAPE>(sc, loc, cl, nl) - (float)ws.r;
+            if (nr < NR && dist < (float)PM_CONTACT_MARGIN_SPHERE) {
+                const V3 n = mul(oR[TGT], nl);
+                offer(RobotCand{geo.wc - n * (float)ws.r, bd[TGT].pos + mul(oR[TGT], cl), n, dist,
+                                (float)ws.mu * sc.fric, ws.link, TGT, WID});
+            }
+        }
+    });
+    return nr;
+}
+
 // STD_MOTORS: the motors are the ones RobotTaskEnv.step sets (POSITION_CONTROL
 // on all nine joints with the fixed Panda gains and forces, panda.py:40-56), so
 // only the targets are per-env; otherwise every gain comes from `mt`.
@@ -1143,17 +1514,33 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             geo.ax[d] = dof_axis<d>(k);
             if constexpr (d < 7) geo.org[d] = k.f[d].o;
         });
-        static_for<0, PM_NUM_SPHERES>([&](auto SS) {
-            constexpr int S = decltype(SS)::value;
-            constexpr SphereDef s = sphere_def(S);
-            geo.spw[S] = k.f[s.link].o + mul(k.f[s.link].R, mk((float)s.c[0], (float)s.c[1], (float)s.c[2])) + sc.base;
+        geo.hR = k.f[8].R;  // links 9 and 10 carry the hand's rotation
+        static_for<0, PM_NUM_BOXES>([&](auto BB) {
+            constexpr int B = decltype(BB)::value;
+            constexpr BoxDef b = box_def(B);
+            geo.bc[B] = k.f[b.link].o + mul(k.f[b.link].R, mk((float)b.c[0], (float)b.c[1], (float)b.c[2])) + sc.base;
         });
+        {
+            constexpr SphereDef w = wrist_def();
+            geo.wc = k.f[w.link].o + mul(k.f[w.link].R, mk((float)w.c[0], (float)w.c[1], (float)w.c[2])) + sc.base;
+        }
         mass_matrix(k, Mi);
     }
     PS_PHASE(1);
     __builtin_amdgcn_sched_barrier(0);
     spd_inverse(Mi);
     PS_PHASE(2);
+    __builtin_amdgcn_sched_barrier(0);
+    // gripper contact candidates: geometry only, so they are found here, where
+    // few registers are live, and wait in LDS (robot_candidates)
+    int nr;
+    {
+        M3 oR[NB];
+#pragma unroll
+        for (int b = 0; b < NB; b++) oR[b] = NOBJ > 0 ? quat_to_mat(bd[b].quat) : M3{{1, 0, 0, 0, 1, 0, 0, 0, 1}};
+        nr = robot_candidates<NOBJ, SHAPE>(sc, geo, bd, oR, lds);
+    }
+    PS_PHASE(17);
     __builtin_amdgcn_sched_barrier(0);
     // M^-1 for the joint rows stays in registers: re-reading it from LDS in
     // every PGS iteration exposed the LDS latency once per motor row (Push
@@ -1391,56 +1778,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         wc.store(PS_F_WPN, (float)np);
     }
     RobotContact rc[NR];
-    int nr = 0;
     {
-        PS_PHASE(17);
-        // 1) candidate gripper contacts in spec order (spheres vs object 1,
-        //    vs object 2, then spheres vs ground) -> small records; the first
-        //    NR active ones are assigned slots 0..NR-1 (select into
-        //    compile-time slots)
-        struct Cand {
-            V3 pA, pB, n;
-            float dist, mu;
-            int link;
-            int obj;  // -1: ground
-            int id;   // cache id: 1 + sphere + 8 * (object, or 2 for the ground)
-        };
-        Cand slot[NR];
-#pragma unroll
-        for (int s = 0; s < NR; s++) slot[s] = Cand{mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 1), 1.0f, 0.0f, 8, -1, 0};
-        auto offer = [&](const Cand &c) {
-#pragma unroll
-            for (int s = 0; s < NR; s++)
-                if (s == nr) slot[s] = c;
-            nr++;
-        };
-#pragma unroll
-        for (int b = 0; b < NOBJ; b++) {
-            static_for<0, PM_NUM_SPHERES>([&](auto SS) {
-                constexpr int S = decltype(SS)::value;
-                constexpr SphereDef s = sphere_def(S);
-                V3 loc = tmul(od[b].R, geo.spw[S] - bd[b].pos);
-                V3 cl, nl;
-                float dist = object_closest<SHAPE>(sc, loc, cl, nl) - (float)s.r;
-                if (nr < NR && dist < (float)PM_CONTACT_MARGIN_SPHERE) {
-                    V3 n = mul(od[b].R, nl);
-                    offer(Cand{geo.spw[S] - n * (float)s.r, bd[b].pos + mul(od[b].R, cl), n, dist,
-                               (float)s.mu * sc.fric, s.link, b, 1 + S + 8 * b});
-                }
-            });
-        }
-        static_for<0, PM_NUM_SPHERES>([&](auto SS) {
-            constexpr int S = decltype(SS)::value;
-            constexpr SphereDef s = sphere_def(S);
-            float top;
-            if (nr < NR && ground_top(sc, geo.spw[S].x, geo.spw[S].y, top)) {
-                float dist = geo.spw[S].z - (float)s.r - top;
-                if (dist < (float)PM_CONTACT_MARGIN_SPHERE) {
-                    V3 pA = geo.spw[S] - mk(0, 0, (float)s.r);
-                    offer(Cand{pA, pA, mk(0, 0, 1), dist, (float)(s.mu * PM_DEFAULT_FRICTION), s.link, -1, 1 + S + 16});
-                }
-            }
-        });
         PS_PHASE(18);
         // 2) rows of each used slot: J (registers), M^-1 J^T (LDS), rhs, bounds;
         //    the normal starts from the cached impulse of the same feature
@@ -1453,7 +1791,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         for (int sl = 0; sl < NR; sl++) {
             RobotContact &c = rc[sl];
             if (sl < nr) {
-                const Cand &cd = slot[sl];
+                const RobotCand cd = RobotCand::load(lds, sl);
                 V3 dirs[3];
                 dirs[0] = cd.n;
                 plane_space(cd.n, dirs[1], dirs[2]);

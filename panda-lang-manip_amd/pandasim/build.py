@@ -67,9 +67,12 @@ _MINREG = ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"]
 
 
 def _one_lane_flags(task: int) -> list:
+    # no _SCHED: with the trackers this clang crashes intermittently in the
+    # scheduler's rematerialisation stage (2 of 8 parallel compiles of a group
+    # object, 7 retries for Stack's one-lane object; see compile_unit)
     if task == TASK_STACK:
-        return _SCHED + _MINREG
-    return _SCHED + _CLAUSE + (_REVERSE if task in (0, 1, 3) else [])
+        return _MINREG
+    return _CLAUSE + (_REVERSE if task in (0, 1, 3) else [])
 
 
 # (object name, source, defines and per-unit flags)
@@ -78,7 +81,7 @@ UNITS = ([("pandasim", "pandasim.hip", [])]
              + _one_lane_flags(t))
             for t in range(6) for c in range(2)]
          + [(f"step_t{t}_c{c}_groups", "step_kernels.hip",
-             [f"-DPS_STEP_TASK={t}", f"-DPS_STEP_CONTROL={c}", "-DPS_STEP_GROUPS=1", "-O1"] + _SCHED)
+             [f"-DPS_STEP_TASK={t}", f"-DPS_STEP_CONTROL={c}", "-DPS_STEP_GROUPS=1", "-O1"])
             for t in range(6) if t != TASK_STACK for c in range(2)]
          + [(f"sim_{n}_{s}", "sim_kernels.hip", [f"-DPS_SIM_NOBJ={n}", f"-DPS_SIM_SHAPE={s}"])
             for n, s in ((0, 0), (1, 0), (1, 1), (2, 0))])
@@ -169,7 +172,22 @@ def build(force: bool = False, verbose: bool = True, variant: str = "", extra=()
         cmd = [hipcc, *flags, *defs, "-c", "-o", obj + ".tmp", os.path.join(CSRC, src)]
         if verbose:
             print(" ".join(cmd), flush=True)
-        subprocess.run(cmd, check=True)
+        # this clang (ROCm 7.2, clang-22) intermittently segfaults in the
+        # AMDGPU scheduler's rematerialisation stage (GCNSchedStrategy
+        # PreRARematStage, a sort over SlotIndex) on the large step kernels
+        # when many jobs run at once; the same command succeeds when re-run.
+        # Only a compiler crash is retried -- a diagnostic fails at once.
+        for attempt in range(8):
+            r = subprocess.run(cmd, capture_output=True, text=True)
+            crashed = r.returncode != 0 and ("Stack dump" in r.stderr or "Segmentation fault" in r.stderr)
+            if not crashed:
+                break
+            print(f"[build] {name}: compiler crash, retrying ({attempt + 1})", flush=True)
+        if r.stdout:
+            print(r.stdout, end="")
+        if r.returncode != 0:
+            print(r.stderr[-4000:], flush=True)
+            raise subprocess.CalledProcessError(r.returncode, cmd)
         os.replace(obj + ".tmp", obj)
         with open(stamp_path(obj), "w") as f:
             f.write(key + "\n")

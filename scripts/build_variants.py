@@ -79,11 +79,9 @@ UNIT_VARIANTS = {
     # -O1)
     "groups_o3": lambda units: [(n, s, [d for d in defs if d != "-O1"]) for n, s, defs in units],
     # the scheduler matrix pruned to one set per object class:
-    # no option on the one-lane objects but Stack's trackers, trackers on the groups
+    # no -mllvm scheduler option on any object
     "pruned": lambda units: [(n, s, [d for d in defs if not d.startswith("-amdgpu-") and not d.startswith("-greedy")
-                                     and d != "-mllvm"] + (_TRK if n.startswith("step_t4_") or n.endswith("_groups")
-                                                           else []))
-                             for n, s, defs in units],
+                                     and d != "-mllvm"]) for n, s, defs in units],
 }
 
 

@@ -47,7 +47,7 @@ def main():
     for n, v in zip(NAMES, buf[:8]):
         print(f"  {n:24s} {v / tot * 100:6.2f} %   {v / waves / steps / 20:10.0f} cyc/substep-equiv")
     if buf[3]:
-        parts = (("joint rows", buf[16]), ("object contacts", buf[17]), ("gripper candidates", buf[18]),
+        parts = (("joint rows", buf[16]), ("object contacts", buf[18]), ("gripper candidates", buf[17]),
                  ("gripper rows", buf[3] - buf[16] - buf[17] - buf[18]))
         print("  rows+contacts split: " + ", ".join(f"{n} {v / buf[3] * 100:.1f} %" for n, v in parts))
     subs = buf[10]  # wave-substeps counted by lane 0 of each wave

@@ -154,32 +154,70 @@ def _model_header():
         return f.read()
 
 
-def test_finger_pad_proxies_sit_on_the_pads():
-    """The finger collision proxies (PM_SPHERE_TABLE: two spheres per finger,
-    the meshes being unavailable) against an independent source in the
-    reference: contact-graspnet's Panda gripper control points
-    (panda_gym/envs/contact_graspnet/gripper_control_points/panda.npy, 20
-    points in the hand frame) put the finger pads at z = 0.0753 .. 0.1053 m
-    from the hand origin and 0.0527 m either side of the centre line with the
-    gripper fully open.  The sphere centres must lie on that pad band (hand
-    z), and with the fingers fully open (0.04 m each) within a sphere radius
-    of the pad's lateral position."""
+def _link_aabbs(h):
+    """{link: (lx, ly, lz)} of PM_LINK_TABLE (the last three numbers of each row)."""
     import re
+    out = {}
+    body = h[h.index("#define PM_LINK_TABLE(X)"):h.index("/* DoF -> link index")]
+    for m in re.finditer(r"X\((\d+),([^)]*)\)", body.replace("\\\n", " ")):
+        vals = [v.strip() for v in m.group(2).split(",")]
+        out[int(m.group(1))] = tuple(float(v) for v in vals[-3:])
+    return out
+
+
+def _boxes(h):
+    import re
+    body = h[h.index("#define PM_BOX_TABLE(X)"):h.index("#define PM_BOX_CONTACTS")]
+    return [tuple(float(v) for v in m.groups()) for m in re.finditer(
+        r"X\((\d+), ([-0-9.]+), ([-0-9.]+), ([-0-9.]+), ([-0-9.]+), ([-0-9.]+), ([-0-9.]+), ([-0-9.]+)\)", body)]
+
+
+def test_gripper_proxies_follow_the_reference_hulls():
+    """The hand and finger constants of include/panda_model.h against the
+    hulls the reference ships (tests/golden/panda_gripper_hulls.npz, from
+    contact_graspnet/gripper_models/panda_gripper/{hand,finger}.stl by
+    tests/golden/make_gripper_golden.py, mapped to the URDF frames):
+      * inertia AABBs (PyBullet derives link inertia from the collision
+        AABB): hand = its hull above the flange plane (z >= 0) + Bullet's
+        1 mm convex margin per side; fingers = the finger hull's extents.
+        The 34 hand vertices below z = 0 are left out for a measured reason:
+        with them the joint-5 KAT's angular velocity is -2.949 instead of the
+        reference's -2.969 +- 1e-3 (DESIGN.md §5);
+      * collision boxes: each finger the finger hull's AABB (link 10 turned by
+        pi about z), the palm the AABB of the hand hull at z >= 0.03;
+      * the obj's fingers, placed fully open, are the same hull at the finger
+        joint origin (z = 0.0584) +- the 0.04 m opening;
+      * the pads cover contact-graspnet's finger control points
+        (gripper_control_points/panda.npy: z = 0.0753 .. 0.1053 m in the hand
+        frame, 0.0527 m either side of the centre line, gripper open)."""
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "panda_gripper_hulls.npz"))
+    hand, finger = g["hand"], g["finger_left"]
     h = _model_header()
-    # finger joint origin z in the hand frame (links 9 and 10: PM_JOINT_PRISMATIC rows)
-    fz = [float(m.group(1)) for m in re.finditer(
-        r"X\((?:9|10), 8, PM_JOINT_PRISMATIC, 0\.0, 0\.0, ([0-9.]+)", h)]
-    assert len(fz) == 2 and fz[0] == fz[1]
-    spheres = [tuple(float(v) for v in m.groups()) for m in re.finditer(
-        r"X\((9|10), ([-0-9.]+), ([-0-9.]+), ([-0-9.]+), ([0-9.]+), ([0-9.]+)\)", h)]
-    assert len(spheres) == 4
-    pad_z, pad_y_open, q_open = (0.0753, 0.1053), 0.0527, 0.04
-    for link, cx, cy, cz, r, mu in spheres:
-        z = fz[0] + cz
-        assert pad_z[0] <= z <= pad_z[1], (link, z)
-        y_open = abs(cy) + q_open  # finger frame y plus the prismatic opening, hand frame
-        assert abs(y_open - pad_y_open) <= r, (link, y_open)
-        assert mu == 1.0  # panda.py:47-48
+    aabb = _link_aabbs(h)
+    up = hand[hand[:, 2] >= 0.0]
+    assert len(up) == 68 and len(hand) == 102
+    assert np.allclose(aabb[8], up.max(0) - up.min(0) + 0.002, atol=1e-4), aabb[8]
+    ext = finger.max(0) - finger.min(0)
+    assert np.allclose(aabb[9], ext, atol=1e-4) and np.allclose(aabb[10], ext, atol=1e-4)
+    boxes = _boxes(h)
+    assert [int(b[0]) for b in boxes] == [9, 10, 8]
+    c, hh = (finger.max(0) + finger.min(0)) / 2, (finger.max(0) - finger.min(0)) / 2
+    assert np.allclose(boxes[0][1:4], c, atol=1e-4) and np.allclose(boxes[0][4:7], hh, atol=1e-4)
+    assert np.allclose(boxes[1][1:4], c * [-1, -1, 1], atol=1e-4) and np.allclose(boxes[1][4:7], hh, atol=1e-4)
+    palm = hand[hand[:, 2] >= 0.03]
+    assert np.allclose(boxes[2][1:4], (palm.max(0) + palm.min(0)) / 2, atol=1e-4)
+    assert np.allclose(boxes[2][4:7], (palm.max(0) - palm.min(0)) / 2, atol=1e-4)
+    assert boxes[0][7] == boxes[1][7] == 1.0 and boxes[2][7] == 0.5  # panda.py:47-48; Bullet's default
+    # the obj's fingers at full opening: the left hull at +y, the right one turned by pi
+    fa, fb = g["obj_finger_a"], g["obj_finger_b"]
+    left, right = (fa, fb) if fa[:, 1].mean() > 0 else (fb, fa)
+    place = lambda f, sy: f * [sy, sy, 1] + [0.0, sy * 0.04, 0.0584]
+    assert np.allclose(np.sort(left, 0), np.sort(place(finger, 1), 0), atol=2e-4)
+    assert np.allclose(np.sort(right, 0), np.sort(place(finger, -1), 0), atol=2e-4)
+    # the pads cover the control points (gripper open, finger joint at z 0.0584)
+    fy0, fy1 = 0.04 + boxes[0][2] - boxes[0][5], 0.04 + boxes[0][2] + boxes[0][5]
+    fz0, fz1 = 0.0584 + boxes[0][3] - boxes[0][6], 0.0584 + boxes[0][3] + boxes[0][6]
+    assert fy0 <= 0.0527 <= fy1 and fz0 <= 0.0753 and 0.1053 <= fz1
 
 
 def test_gymnasium_registration_mirrors_the_reference(monkeypatch):
