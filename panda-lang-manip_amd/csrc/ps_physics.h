@@ -689,21 +689,25 @@ PS_D int pick_two(Visit &&visit, V3 org, V3 axis, RCand &c0, RCand &c1) {
     const float margin = (float)PM_CONTACT_MARGIN_ROBOT;
     bool has0 = false, has1 = false;
     c0 = c1 = RCand{mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 1), 1.0f};
+    auto sel = [](bool t, const RCand &a, const RCand &b) {
+        return RCand{t ? a.pA : b.pA, t ? a.pB : b.pB, t ? a.n : b.n, t ? a.dist : b.dist};
+    };
+    // validity folded into the distance (see BoxCube::pick)
+    c0.dist = 1e30f;
     visit([&](bool ok, const RCand &c) {
-        if (ok && c.dist < margin && (!has0 || c.dist < c0.dist)) {
-            c0 = c;
-            has0 = true;
-        }
+        const float de = ok ? c.dist : 1e30f;
+        const bool take = de < fminf(margin, c0.dist);
+        c0 = sel(take, c, c0);
     });
-    float best = 1e-8f;  // (0.1 mm)^2
+    has0 = c0.dist < margin;
+    float best = has0 ? 1e-8f : 1e30f;  // (0.1 mm)^2
     visit([&](bool ok, const RCand &c) {
         const V3 d = c.pA - c0.pA;
         const float d2 = dot(d, d);
-        if (has0 && ok && c.dist < margin && d2 > best) {
-            best = d2;
-            c1 = c;
-            has1 = true;
-        }
+        const bool take = (ok ? c.dist : 1e30f) < margin && d2 > best;
+        best = take ? d2 : best;
+        c1 = sel(take, c, c1);
+        has1 = has1 || take;
     });
     if (has1 && dot(c1.pA - org, axis) < dot(c0.pA - org, axis)) {
         const RCand t = c0;
@@ -785,12 +789,10 @@ struct BoxCube {
             P[q][2] = dot(rel, nref);
         }
     }
+    // the candidates in the reference face's frame: (ok, u, v, depth), from
+    // the incident face P and the rectangle half extents hu, hv
     template <class F>
-    PS_D void visit(F &&f) const {
-        auto emit = [&](bool ok, float u, float v, float depth) {
-            const V3 pref = cf + t1 * u + t2 * v, pinc = pref + nref * depth;
-            f(ok && !sep, RCand{robot_ref ? pref : pinc, robot_ref ? pinc : pref, robot_ref ? -nref : nref, depth});
-        };
+    PS_D static void visit(const float (&P)[4][3], float hu, float hv, F &&emit) {
         constexpr float cu[4] = {-1, 1, 1, -1}, cv[4] = {-1, -1, 1, 1};
         // 1. incident vertices inside the reference rectangle
 #pragma unroll
@@ -799,6 +801,8 @@ struct BoxCube {
         const float e1u = P[1][0] - P[0][0], e1v = P[1][1] - P[0][1], e1d = P[1][2] - P[0][2];
         const float e3u = P[3][0] - P[0][0], e3v = P[3][1] - P[0][1], e3d = P[3][2] - P[0][2];
         const float pnu = e1v * e3d - e1d * e3v, pnv = e1d * e3u - e1u * e3d, pnd = e1u * e3v - e1v * e3u;
+        const bool okp = pnd != 0.0f;
+        const float ipnd = okp ? 1.0f / pnd : 0.0f;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const float u = cu[q] * hu, v = cv[q] * hv;
@@ -810,26 +814,85 @@ struct BoxCube {
                 pos = pos && cr >= 0.0f;
                 neg = neg && cr <= 0.0f;
             }
-            const bool okp = pnd != 0.0f;
-            const float depth = okp ? P[0][2] - (pnu * (u - P[0][0]) + pnv * (v - P[0][1])) / pnd : 0.0f;
+            const float depth = okp ? P[0][2] - (pnu * (u - P[0][0]) + pnv * (v - P[0][1])) * ipnd : 0.0f;
             emit((pos || neg) && okp, u, v, depth);
         }
         // 3. incident edges crossing the rectangle's edges (u = +-hu, v = +-hv)
 #pragma unroll
         for (int e = 0; e < 4; e++) {
             const int e2 = (e + 1) & 3;
+            const float du = P[e2][0] - P[e][0], dv = P[e2][1] - P[e][1], dd = P[e2][2] - P[e][2];
+            const float idu = du != 0.0f ? 1.0f / du : 0.0f, idv = dv != 0.0f ? 1.0f / dv : 0.0f;
 #pragma unroll
             for (int s = 0; s < 4; s++) {
                 const bool on_u = s < 2;
                 const float lim = (s & 1) ? -(on_u ? hu : hv) : (on_u ? hu : hv);
-                const float ca = on_u ? P[e][0] : P[e][1], cb = on_u ? P[e2][0] : P[e2][1];
-                const float den = cb - ca;
-                const float t = den != 0.0f ? (lim - ca) / den : -1.0f;
-                const float u = P[e][0] + t * (P[e2][0] - P[e][0]), v = P[e][1] + t * (P[e2][1] - P[e][1]);
+                const float ca = on_u ? P[e][0] : P[e][1];
+                const bool has = on_u ? du != 0.0f : dv != 0.0f;
+                const float t = has ? (lim - ca) * (on_u ? idu : idv) : -1.0f;
+                const float u = P[e][0] + t * du, v = P[e][1] + t * dv;
                 const bool ok = t > 0.0f && t < 1.0f && (on_u ? fabsf(v) <= hv : fabsf(u) <= hu);
-                emit(ok, on_u ? lim : u, on_u ? v : lim, P[e][2] + t * (P[e2][2] - P[e][2]));
+                emit(ok, on_u ? lim : u, on_u ? v : lim, P[e][2] + t * dd);
             }
         }
+    }
+    PS_D RCand to_world(float u, float v, float depth) const {
+        const V3 pref = cf + t1 * u + t2 * v, pinc = pref + nref * depth;
+        return RCand{robot_ref ? pref : pinc, robot_ref ? pinc : pref, robot_ref ? -nref : nref, depth};
+    }
+    // pick_two over the candidates, in the reference face's frame: the robot
+    // point's offsets are (du, dv) when the box is the reference, (du, dv,
+    // ddepth) when it is the incident one; only the two picks go to world
+    PS_D int pick(V3 org, V3 axis, RCand &c0, RCand &c1) const {
+        const float margin = (float)PM_CONTACT_MARGIN_ROBOT;
+        const float wd = robot_ref ? 0.0f : 1.0f;
+        bool has0 = false, has1 = false;
+        float u0 = 0.0f, v0 = 0.0f, d0 = 1e30f, u1 = 0.0f, v1 = 0.0f, d1 = 1.0f;
+        // Branch-free selects, validity folded into the depth (+inf): kept as
+        // lane masks, the candidates' 24 validity bits stayed live in SGPRs
+        // across both passes and spilled ~900 of them to VGPR lanes per
+        // substep.  Pass 2 recomputes the candidates from an opaque copy of
+        // the face (no common subexpressions between the passes).
+        float Q[4][3];
+        float qu = hu, qv = hv;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int k = 0; k < 3; k++) Q[q][k] = P[q][k];
+        visit(Q, qu, qv, [&](bool ok, float u, float v, float d) {
+            const float de = ok ? d : 1e30f;
+            const bool take = de < fminf(margin, d0);
+            u0 = take ? u : u0;
+            v0 = take ? v : v0;
+            d0 = take ? de : d0;
+        });
+        has0 = d0 < margin;
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int k = 0; k < 3; k++) asm volatile("" : "+v"(Q[q][k]));
+        asm volatile("" : "+v"(qu), "+v"(qv));
+        float best = has0 ? 1e-8f : 1e30f;  // (0.1 mm)^2
+        visit(Q, qu, qv, [&](bool ok, float u, float v, float d) {
+            const float eu = u - u0, ev = v - v0, ed = (d - d0) * wd;
+            const float e2 = eu * eu + ev * ev + ed * ed;
+            const bool take = (ok ? d : 1e30f) < margin && e2 > best;
+            best = take ? e2 : best;
+            u1 = take ? u : u1;
+            v1 = take ? v : v1;
+            d1 = take ? d : d1;
+            has1 = has1 || take;
+        });
+        has0 = has0 && !sep;
+        has1 = has1 && has0;
+        c0 = to_world(u0, v0, d0);
+        c1 = to_world(u1, v1, d1);
+        if (has1 && dot(c1.pA - org, axis) < dot(c0.pA - org, axis)) {
+            const RCand t = c0;
+            c0 = c1;
+            c1 = t;
+        }
+        return has0 ? (has1 ? 2 : 1) : 0;
     }
 };
 
@@ -940,9 +1003,10 @@ struct BoxCyl {
 // robot box vs the ground (table top or plane)
 template <class F>
 PS_D void box_ground_visit(const Scene &sc, V3 xc, const M3 &xR, V3 xh, F &&f) {
+    const V3 ea = col(xR, 0) * xh.x, eb = col(xR, 1) * xh.y, ec = col(xR, 2) * xh.z;
 #pragma unroll
     for (int v = 0; v < 8; v++) {
-        const V3 p = xc + mul(xR, mk((v & 1) ? xh.x : -xh.x, (v & 2) ? xh.y : -xh.y, (v & 4) ? xh.z : -xh.z));
+        const V3 p = xc + ((v & 1) ? ea : -ea) + ((v & 2) ? eb : -eb) + ((v & 4) ? ec : -ec);
         float top = 0.0f;
         const bool ok = ground_top(sc, p.x, p.y, top);
         f(ok, RCand{p, mk(p.x, p.y, top), mk(0, 0, 1), p.z - top});
@@ -1456,7 +1520,7 @@ PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const
                 ns = pick_two([&](auto &&f) { bcy.visit(sc, f); }, xc, axis, c0, c1);
             } else {
                 const BoxCube bcu(xc, geo.hR, xh, bd[TGT].pos, oR[TGT], sc.half);
-                ns = pick_two([&](auto &&f) { bcu.visit(f); }, xc, axis, c0, c1);
+                ns = bcu.pick(xc, axis, c0, c1);
             }
             const float mu = (float)bx.mu * (GROUND ? (float)PM_DEFAULT_FRICTION : sc.fric);
             const int obj = GROUND ? -1 : TGT;
