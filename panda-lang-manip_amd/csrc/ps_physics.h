@@ -1513,14 +1513,31 @@ PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const
             RCand c0, c1;
             int ns = 0;
             const V3 axis = col(geo.hR, box_long_axis(B));
+            // a conservative bounding test first (no candidate of a pair that
+            // fails it is within the margin, so the picks are unchanged): the
+            // block is skipped when no lane of the wave passes it -- the palm
+            // is almost never near the table or the object
+            constexpr float rbox = (float)(bx.h[0] + bx.h[1] + bx.h[2]) + (float)PM_CONTACT_MARGIN_ROBOT;
+            bool near;
             if constexpr (GROUND) {
-                ns = pick_two([&](auto &&f) { box_ground_visit(sc, xc, geo.hR, xh, f); }, xc, axis, c0, c1);
-            } else if constexpr (SHAPE == SHAPE_CYL) {
-                const BoxCyl bcy(sc, xc, geo.hR, xh, bd[TGT].pos, oR[TGT]);
-                ns = pick_two([&](auto &&f) { bcy.visit(sc, f); }, xc, axis, c0, c1);
+                const V3 ea = col(geo.hR, 0) * xh.x, eb = col(geo.hR, 1) * xh.y, ec = col(geo.hR, 2) * xh.z;
+                const float low = xc.z - (fabsf(ea.z) + fabsf(eb.z) + fabsf(ec.z));
+                near = low < (float)PM_TABLE_TOP + (float)PM_CONTACT_MARGIN_ROBOT;  // the highest ground
             } else {
-                const BoxCube bcu(xc, geo.hR, xh, bd[TGT].pos, oR[TGT], sc.half);
-                ns = bcu.pick(xc, axis, c0, c1);
+                const V3 d = xc - bd[TGT].pos;
+                const float robj = SHAPE == SHAPE_CYL ? sc.half.x + sc.half.z : sc.half.x + sc.half.y + sc.half.z;
+                near = dot(d, d) < (rbox + robj) * (rbox + robj);
+            }
+            if (near) {
+                if constexpr (GROUND) {
+                    ns = pick_two([&](auto &&f) { box_ground_visit(sc, xc, geo.hR, xh, f); }, xc, axis, c0, c1);
+                } else if constexpr (SHAPE == SHAPE_CYL) {
+                    const BoxCyl bcy(sc, xc, geo.hR, xh, bd[TGT].pos, oR[TGT]);
+                    ns = pick_two([&](auto &&f) { bcy.visit(sc, f); }, xc, axis, c0, c1);
+                } else {
+                    const BoxCube bcu(xc, geo.hR, xh, bd[TGT].pos, oR[TGT], sc.half);
+                    ns = bcu.pick(xc, axis, c0, c1);
+                }
             }
             const float mu = (float)bx.mu * (GROUND ? (float)PM_DEFAULT_FRICTION : sc.fric);
             const int obj = GROUND ? -1 : TGT;
