@@ -25,6 +25,25 @@ extern "C" int ps_debug_phase_cycles(unsigned long long *out, int reset) {
 }
 #endif
 
+#ifdef PS_DEBUG_ROW_DUMP
+// row dump of the diagnostic build (KParams::dbg): PS_DUMP_LANES lanes x 2
+// substeps x PS_DUMP_ROWS floats, NaN where nothing was recorded
+static float *g_dump = nullptr;
+static const size_t kDumpFloats = (size_t)PS_DUMP_LANES * 2 * PS_DUMP_ROWS;
+float *ps_row_dump_buffer() {
+    if (!g_dump && hipMalloc((void **)&g_dump, sizeof(float) * kDumpFloats) == hipSuccess)
+        (void)hipMemset(g_dump, 0xFF, sizeof(float) * kDumpFloats);
+    return g_dump;
+}
+extern "C" int ps_debug_row_dump(float *out, int reset) {
+    float *b = ps_row_dump_buffer();
+    if (!b || hipDeviceSynchronize() != hipSuccess) return PS_ERR_HIP;
+    if (hipMemcpy(out, b, sizeof(float) * kDumpFloats, hipMemcpyDeviceToHost) != hipSuccess) return PS_ERR_HIP;
+    if (reset && hipMemset(b, 0xFF, sizeof(float) * kDumpFloats) != hipSuccess) return PS_ERR_HIP;
+    return PS_OK;
+}
+#endif
+
 namespace {
 
 // ---------------------------------------------------------------- kernels

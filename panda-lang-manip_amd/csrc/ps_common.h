@@ -46,6 +46,21 @@ struct PhaseTimer {
 #define PS_PHASE(k) do {} while (0)
 #endif
 
+// Row dump (diagnostic build only, -DPS_DEBUG_ROW_DUMP; scripts/row_dump.py):
+// the group solver's inputs and the impulse change of every row of the first
+// PGS iteration pair of substeps 0 and 1, per lane, PS_DUMP_ROWS floats per
+// lane and substep (the -O3 group-kernel investigation).
+// Compiled out of the product.
+#define PS_DUMP_ROWS 256
+#define PS_DUMP_LANES 4096  // lanes dumped (the first 4 096 of the grid)
+#ifdef PS_DEBUG_ROW_DUMP
+#define PS_DUMP_PARAM , float *dump
+#define PS_DUMP_ARG , dump
+#else
+#define PS_DUMP_PARAM
+#define PS_DUMP_ARG
+#endif
+
 namespace ps {
 
 // ------------------------------------------------------------------ vectors

@@ -74,6 +74,9 @@ PS_DECLARE_SIM_LAUNCHER(2, 0)
 #ifdef PS_PROFILE_PHASES
 unsigned long long *ps_prof_buffer();
 #endif
+#ifdef PS_DEBUG_ROW_DUMP
+float *ps_row_dump_buffer();
+#endif
 
 // minimum waves per SIMD the step kernels are register-allocated for
 #ifndef PS_STEP_MIN_WAVES
@@ -165,6 +168,9 @@ struct KParams {
     int64_t epstride;
 #ifdef PS_PROFILE_PHASES
     unsigned long long *prof;  // phase counters (ps_prof_buffer)
+#endif
+#ifdef PS_DEBUG_ROW_DUMP
+    float *dbg;  // row dump (ps_row_dump_buffer)
 #endif
 };
 
@@ -286,7 +292,12 @@ PS_D void run_substeps(const KParams &P, int64_t i, int n, float q[9], float qd[
         } else {
             load_motors(P.s, ii, m);
         }
-        substep<NOBJ, SHAPE, STD_MOTORS, G>(P.sc, q, qd, m, bd, lds, wc PS_PROF_ARG);
+#ifdef PS_DEBUG_ROW_DUMP
+        float *dump = (P.dbg && st < 2 && ((uint64_t)blockIdx.x * 64 + __lane_id()) < PS_DUMP_LANES)
+                          ? P.dbg + (((uint64_t)blockIdx.x * 64 + __lane_id()) * 2 + st) * PS_DUMP_ROWS
+                          : nullptr;
+#endif
+        substep<NOBJ, SHAPE, STD_MOTORS, G>(P.sc, q, qd, m, bd, lds, wc PS_PROF_ARG PS_DUMP_ARG);
     }
     wc.from_lds();
 }
@@ -573,6 +584,9 @@ inline KParams params_of(ps_ctx *c, void *state) {
     P.epstride = c->num_envs;
 #ifdef PS_PROFILE_PHASES
     P.prof = ps_prof_buffer();
+#endif
+#ifdef PS_DEBUG_ROW_DUMP
+    P.dbg = ps_row_dump_buffer();
 #endif
     return P;
 }

@@ -1262,8 +1262,30 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
                     unsigned lim_on, unsigned gate_gnd, unsigned gate_robot, const float dinvj[9],
                     const float lim_rhs[9], float lim_lam[9], const float mot_rhs[9], float mot_lam[9],
                     GroundContact gc[NG], RobotContact rc[NR], const BodyDyn<SHAPE> &od, float gmu, float dv[9],
-                    V3 &dw, V3 &dvl PS_PROF_COUNT_PARAM) {
+                    V3 &dw, V3 &dvl PS_PROF_COUNT_PARAM PS_DUMP_PARAM) {
     static_assert((G == 16 || G == 8) && NOBJ <= 1, "groups of 16 or 8 lanes hold 9 robot + 6 object DoFs");
+#ifdef PS_DEBUG_ROW_DUMP
+    int dk = 0;
+    auto rec = [&](float x) {
+        if (dump && dk < PS_DUMP_ROWS) dump[dk] = x;
+        dk++;
+    };
+#pragma unroll
+    for (int d = 0; d < 9; d++) { rec(mot_rhs[d]); rec(dinvj[d]); rec(lim_rhs[d]); }
+#pragma unroll
+    for (int c = 0; c < NG; c++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) { rec(gc[c].rhs[j]); rec(gc[c].dinv[j]); }
+#pragma unroll
+    for (int c = 0; c < NR; c++)
+#pragma unroll
+        for (int j = 0; j < 3; j++) { rec(rc[c].rhs[j]); rec(rc[c].dinv[j]); rec(rc[c].lam[j]); }
+    rec(__builtin_bit_cast(float, gate_lim | (gate_gnd << 9) | (gate_robot << 13)));
+    bool dump_on = dump != nullptr;
+#define PS_REC(x) do { if (dump_on) rec(x); } while (0)
+#else
+#define PS_REC(x) do {} while (0)
+#endif
     constexpr int K = 16 / G;  // DoFs per lane
     const int e = (int)(__lane_id() & (unsigned)(G - 1));
     // lane e's slices: rows e + k G of M^-1 (joint rows), object-only rows, robot rows
@@ -1361,6 +1383,7 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         float nl = fminf(fmaxf(lam + dl, lo), hi);
         dl = nl - lam;
         lam = nl;
+        PS_REC(dl);
 #pragma unroll
         for (int k = 0; k < K; k++) dvm[k] = fmaf(mrow[k][d], sgn * dl, dvm[k]);
         res = fmaxf(res, joint_viol(dl, midg[d]));
@@ -1387,6 +1410,7 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         float nl = fminf(fmaxf(lam + dl, 0.0f), (float)PM_CONTACT_UPPER);
         dl = nl - lam;
         lam = nl;
+        PS_REC(dl);
         apply(Mm, dl);
         res = fmaxf(res, row_viol(dl, dinv));
     };
@@ -1403,6 +1427,8 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         dlb = b - lam[2];
         lam[1] = a;
         lam[2] = b;
+        PS_REC(dla);
+        PS_REC(dlb);
 #pragma unroll
         for (int k = 0; k < K; k++) dvm[k] = fmaf(M[2][k], dlb, fmaf(M[1][k], dla, dvm[k]));
         res = fmaxf(res, fmaxf(row_viol(dla, dinv[1]), row_viol(dlb, dinv[2])));
@@ -1446,8 +1472,13 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         up(motor_row);
         ground_normals();
         contacts();
+#ifdef PS_DEBUG_ROW_DUMP
+        rec(res);
+        dump_on = false;
+#endif
         if (res <= 0.0f) break;
     }
+#undef PS_REC
     // every lane of the group gets the whole velocity change
     static_for<0, 9>([&](auto DD) {
         constexpr int d = decltype(DD)::value;
@@ -1574,7 +1605,7 @@ PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const
 // only the targets are per-env; otherwise every gain comes from `mt`.
 template <int NOBJ, int SHAPE, bool STD_MOTORS, int G = 1>
 PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Body *bd, const MJStore &lds,
-                  const WarmCache<G, NOBJ> &wc PS_PROF_PARAM) {
+                  const WarmCache<G, NOBJ> &wc PS_PROF_PARAM PS_DUMP_PARAM) {
     static_assert(NOBJ >= 0 && NOBJ <= 2, "objects");
     static_assert(NOBJ < 2 || SHAPE == SHAPE_BOX, "Stack stacks cubes");
     constexpr int NB = NOBJ > 0 ? NOBJ : 1;  // array extents
@@ -2513,7 +2544,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     } else {
         group_pgs<NOBJ, SHAPE, STD_MOTORS, G>(mt, Mi, lds, gate_lim, lim_up, lim_on, gate_ground[0], gate_robot,
                                               dinvj, lim_rhs, lim_lam, mot_rhs, mot_lam, gc[0], rc, od[0], gmu,
-                                              dv, dw[0], dvl[0] PS_PROF_COUNT_ARG);
+                                              dv, dw[0], dvl[0] PS_PROF_COUNT_ARG PS_DUMP_ARG);
     }
 
     // the contacts' final normal impulses become the cache of the next

@@ -27,6 +27,10 @@ VARIANTS = {
     "o1": ["-O1"],
     "prealloc": ["-mllvm", "-amdgpu-prealloc-sgpr-spill-vgprs=1"],
     "nodppc": ["-mllvm", "-amdgpu-dpp-combine=0"],
+    # the group solver's row dump (scripts/row_dump.py): product objects, and
+    # the group objects at -O3
+    "dump": ["-DPS_DEBUG_ROW_DUMP"],
+    "groups_o3_dump": ["-DPS_DEBUG_ROW_DUMP"],
 }
 
 
@@ -78,6 +82,7 @@ UNIT_VARIANTS = {
     # the group-kernel objects at the library's -O3 (the product builds them at
     # -O1)
     "groups_o3": lambda units: [(n, s, [d for d in defs if d != "-O1"]) for n, s, defs in units],
+    "groups_o3_dump": lambda units: [(n, s, [d for d in defs if d != "-O1"]) for n, s, defs in units],
     # the scheduler matrix pruned to one set per object class:
     # no -mllvm scheduler option on any object
     "pruned": lambda units: [(n, s, [d for d in defs if not d.startswith("-amdgpu-") and not d.startswith("-greedy")
