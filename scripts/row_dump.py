@@ -40,7 +40,7 @@ np.savez(out, dump=buf.reshape(4096, 2, 256), q=env.sim.f[0:18, :B].double().cpu
 def main(task, control, lanes, libs):
     res = []
     for i, lib in enumerate(libs):
-        out = os.path.join(ROOT, "gpurun_out", f"row_dump_{task}_{control}_{lanes}_{i}.npz")
+        out = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"row_dump_{task}_{control}_{lanes}_{i}.npz")  # 8 MB each: not under gpurun_out
         env = dict(os.environ, PANDASIM_LIB=os.path.abspath(lib), ROOT=ROOT)
         p = subprocess.run([sys.executable, "-c", CHILD, task, control, str(lanes), out], env=env,
                            capture_output=True, text=True, timeout=300)
