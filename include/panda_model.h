@@ -149,8 +149,15 @@
  * Link 7 (PyBullet link 6, "panda_link7", no mesh in the reference) keeps a
  * sphere proxy of the wrist body above the flange (PM_WRIST_SPHERE).
  * Contacts are offered per object, then for the ground, in the order boxes
- * (fingers first), wrist: at most PM_BOX_CONTACTS per box and target
- * (DESIGN.md §5), PM_MAX_ROBOT_CONTACTS in all.
+ * (fingers first), wrist: at most PM_BOX_CONTACTS per box and object, one per
+ * box on the ground (the arm's motors hold the hand's orientation; a finger
+ * pad on an object needs two to resist a twist),
+ * PM_MAX_ROBOT_CONTACTS in all.
+ * Picking the points: the first minimises depth + PM_PICK_SKEW_WEIGHT x the
+ * point's coordinate along PM_PICK_SKEW (box frame) -- the skew term decides
+ * among near-equal depths, a face lying flat on a face, where the deepest
+ * point alone is decided by rounding; the second is the candidate farthest
+ * from the first; the two are ordered along PM_PICK_SKEW.
  */
 #define PM_NUM_BOXES 3
 #define PM_BOX_TABLE(X)                                                  \
@@ -158,6 +165,11 @@
     X(10, 0.0, -0.0131, 0.0270, 0.0105, 0.0133, 0.0269, 1.0)            \
     X(8, 0.0007, 0.0001, 0.0481, 0.0200, 0.1004, 0.0178, 0.5)
 #define PM_BOX_CONTACTS 2
+#define PM_BOX_GROUND_CONTACTS 1
+#define PM_PICK_SKEW_X 0.8
+#define PM_PICK_SKEW_Y 0.5
+#define PM_PICK_SKEW_Z 0.3
+#define PM_PICK_SKEW_WEIGHT 0.01
 /* X(link, cx, cy, cz, radius, lateral_friction) */
 #define PM_WRIST_SPHERE(X) X(6, 0.0, 0.0, 0.060, 0.050, 0.5)
 #define PM_CONTACT_MARGIN_ROBOT 0.005

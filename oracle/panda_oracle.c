@@ -827,10 +827,13 @@ static void box_box_contacts(const po_config *cfg, const po_env *env, const oobj
  *     on the curved side: its two ends), and the cylinder's 16 rim points
  *     against the box;
  *   box vs ground: the box's 8 vertices.
- * Of the candidates within PM_CONTACT_MARGIN_ROBOT the deepest is taken, then
- * the one farthest from it (0.1 mm apart at least); the two are ordered along
- * the box's longest axis, which makes the order (the contact's cache id) a
- * property of the geometry.  A is the robot, B the object or ground, n points
+ * Of the candidates within PM_CONTACT_MARGIN_ROBOT the one minimising depth +
+ * PM_PICK_SKEW_WEIGHT x its coordinate along PM_PICK_SKEW (box frame) is taken
+ * (the skew term decides among near-equal depths: a fingertip lying flat on
+ * the table, where the deepest corner alone would be decided by rounding),
+ * then -- for an object, not the ground -- the one farthest from it (0.1 mm
+ * apart at least); the two are ordered along PM_PICK_SKEW, which makes the
+ * order (the contact's cache id) a property of the geometry.  A is the robot, B the object or ground, n points
  * from B to A. */
 typedef struct {
     double pA[3], pB[3], n[3], dist;
@@ -856,13 +859,22 @@ static void robot_box(const okin *k, int b, double c[3], double R[9]) {
     memcpy(R, k->R[d->link], sizeof(double) * 9);
 }
 
-static int longest_axis(const double h[3]) { return h[2] >= h[1] && h[2] >= h[0] ? 2 : (h[1] >= h[0] ? 1 : 0); }
-
-static int pick_contacts(const ocand *cand, int m, const double bc[3], const double bR[9], int ax, ocand out[2]) {
+static int pick_contacts(const ocand *cand, int m, const double bc[3], const double bR[9], int maxn, ocand out[2]) {
+    /* the skew direction PM_PICK_SKEW in the box's frame, world */
+    const double wl[3] = {PM_PICK_SKEW_X, PM_PICK_SKEW_Y, PM_PICK_SKEW_Z};
+    double w[3];
+    m3_vec(bR, wl, w);
     int first = -1;
-    for (int i = 0; i < m; i++)
-        if (cand[i].dist < PM_CONTACT_MARGIN_ROBOT && (first < 0 || cand[i].dist < cand[first].dist)) first = i;
+    double fs = 0.0;
+    for (int i = 0; i < m; i++) {
+        if (!(cand[i].dist < PM_CONTACT_MARGIN_ROBOT)) continue;
+        double r[3] = {cand[i].pA[0] - bc[0], cand[i].pA[1] - bc[1], cand[i].pA[2] - bc[2]};
+        double sc = cand[i].dist + PM_PICK_SKEW_WEIGHT * v3_dot(r, w);
+        if (first < 0 || sc < fs) { first = i; fs = sc; }
+    }
     if (first < 0) return 0;
+    out[0] = cand[first];
+    if (maxn < 2) return 1;
     int second = -1;
     double best = 1e-8; /* (0.1 mm)^2 */
     for (int i = 0; i < m; i++) {
@@ -871,12 +883,11 @@ static int pick_contacts(const ocand *cand, int m, const double bc[3], const dou
         for (int j = 0; j < 3; j++) d2 += (cand[i].pA[j] - cand[first].pA[j]) * (cand[i].pA[j] - cand[first].pA[j]);
         if (d2 > best) { best = d2; second = i; }
     }
-    out[0] = cand[first];
     if (second < 0) return 1;
     out[1] = cand[second];
-    double axis[3] = {bR[ax], bR[3 + ax], bR[6 + ax]}, r0[3], r1[3];
+    double r0[3], r1[3];
     for (int j = 0; j < 3; j++) { r0[j] = out[0].pA[j] - bc[j]; r1[j] = out[1].pA[j] - bc[j]; }
-    if (v3_dot(r1, axis) < v3_dot(r0, axis)) {
+    if (v3_dot(r1, w) < v3_dot(r0, w)) {
         ocand t = out[0];
         out[0] = out[1];
         out[1] = t;
@@ -1083,9 +1094,11 @@ static int box_cyl_cands(const po_config *cfg, const double xc[3], const double 
             OL_PUSH();
         }
     }
-    /* 3. rim points vs the box */
+    /* 3. rim points vs the box -- only for a box with a half extent beyond the
+     *    radius (the palm): a narrower box's face inside a cap is found by its
+     *    own vertices (1) */
     double pts[2 * PM_CYL_RIM_POINTS][3];
-    int np = object_support_points(cfg, pts);
+    int np = (xh[0] > r || xh[1] > r || xh[2] > r) ? object_support_points(cfg, pts) : 0;
     for (int p = 0; p < np; p++) {
         double dl[3] = {pts[p][0] - bc[0], pts[p][1] - bc[1], pts[p][2] - bc[2]}, lp[3], cl[3], dif[3];
         m3_tvec(bR, dl, lp); /* rim point in the box frame */
@@ -1215,7 +1228,7 @@ static int gen_contacts(const po_config *cfg, const po_env *env, const okin *k, 
                     m = box_cyl_cands(cfg, xc, xR, BOXES[bx].h, env->obj[tgt].pos, ob[tgt].R, cand);
                 else
                     m = box_cube_cands(xc, xR, BOXES[bx].h, env->obj[tgt].pos, ob[tgt].R, cfg->object_half, cand);
-                int ns = pick_contacts(cand, m, xc, xR, longest_axis(BOXES[bx].h), sel);
+                int ns = pick_contacts(cand, m, xc, xR, ground ? PM_BOX_GROUND_CONTACTS : PM_BOX_CONTACTS, sel);
                 for (int q = 0; q < ns && nr < PM_MAX_ROBOT_CONTACTS; q++) {
                     ocontact *c = &out[nc++];
                     nr++;

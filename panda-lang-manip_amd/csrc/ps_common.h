@@ -246,13 +246,6 @@ PS_HD constexpr SphereDef wrist_def() {
     const SphereDef t[1] = {PM_WRIST_SPHERE(PS_SPHDEF)};
     return t[0];
 }
-// the box's longest axis (the order of its two contact points)
-PS_HD constexpr int box_long_axis(int b) {
-    return box_def(b).h[2] >= box_def(b).h[1] && box_def(b).h[2] >= box_def(b).h[0]
-               ? 2
-               : (box_def(b).h[1] >= box_def(b).h[0] ? 1 : 0);
-}
-
 PS_HD constexpr double joint_force(int d) {
     const double f[PM_NUM_DOFS] = PM_JOINT_FORCES;
     return f[d];

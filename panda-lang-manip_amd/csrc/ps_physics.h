@@ -684,35 +684,39 @@ struct RCand {
 PS_D float comp(V3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
 PS_D V3 colsel(const M3 &R, int c) { return c == 0 ? col(R, 0) : (c == 1 ? col(R, 1) : col(R, 2)); }
 
-template <class Visit>
-PS_D int pick_two(Visit &&visit, V3 org, V3 axis, RCand &c0, RCand &c1) {
+template <int MAXN, class Visit>
+PS_D int pick_two(Visit &&visit, V3 org, V3 w, RCand &c0, RCand &c1) {
     const float margin = (float)PM_CONTACT_MARGIN_ROBOT;
     bool has0 = false, has1 = false;
     c0 = c1 = RCand{mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 1), 1.0f};
     auto sel = [](bool t, const RCand &a, const RCand &b) {
         return RCand{t ? a.pA : b.pA, t ? a.pB : b.pB, t ? a.n : b.n, t ? a.dist : b.dist};
     };
-    // validity folded into the distance (see BoxCube::pick)
-    c0.dist = 1e30f;
+    // validity folded into the score (see BoxCube::pick); the first pick
+    // minimises depth + PM_PICK_SKEW_WEIGHT x the coordinate along the skew
+    float s0 = 1e30f;
     visit([&](bool ok, const RCand &c) {
-        const float de = ok ? c.dist : 1e30f;
-        const bool take = de < fminf(margin, c0.dist);
+        const float sc = (ok && c.dist < margin) ? fmaf((float)PM_PICK_SKEW_WEIGHT, dot(c.pA - org, w), c.dist) : 1e30f;
+        const bool take = sc < s0;
+        s0 = take ? sc : s0;
         c0 = sel(take, c, c0);
     });
-    has0 = c0.dist < margin;
-    float best = has0 ? 1e-8f : 1e30f;  // (0.1 mm)^2
-    visit([&](bool ok, const RCand &c) {
-        const V3 d = c.pA - c0.pA;
-        const float d2 = dot(d, d);
-        const bool take = (ok ? c.dist : 1e30f) < margin && d2 > best;
-        best = take ? d2 : best;
-        c1 = sel(take, c, c1);
-        has1 = has1 || take;
-    });
-    if (has1 && dot(c1.pA - org, axis) < dot(c0.pA - org, axis)) {
-        const RCand t = c0;
-        c0 = c1;
-        c1 = t;
+    has0 = s0 < 1e29f;
+    if constexpr (MAXN >= 2) {
+        float best = has0 ? 1e-8f : 1e30f;  // (0.1 mm)^2
+        visit([&](bool ok, const RCand &c) {
+            const V3 d = c.pA - c0.pA;
+            const float d2 = dot(d, d);
+            const bool take = (ok ? c.dist : 1e30f) < margin && d2 > best;
+            best = take ? d2 : best;
+            c1 = sel(take, c, c1);
+            has1 = has1 || take;
+        });
+        if (has1 && dot(c1.pA - org, w) < dot(c0.pA - org, w)) {
+            const RCand t = c0;
+            c0 = c1;
+            c1 = t;
+        }
     }
     return has0 ? (has1 ? 2 : 1) : 0;
 }
@@ -843,11 +847,15 @@ struct BoxCube {
     // pick_two over the candidates, in the reference face's frame: the robot
     // point's offsets are (du, dv) when the box is the reference, (du, dv,
     // ddepth) when it is the incident one; only the two picks go to world
-    PS_D int pick(V3 org, V3 axis, RCand &c0, RCand &c1) const {
+    PS_D int pick(V3 org, V3 w, RCand &c0, RCand &c1) const {
         const float margin = (float)PM_CONTACT_MARGIN_ROBOT;
         const float wd = robot_ref ? 0.0f : 1.0f;
         bool has0 = false, has1 = false;
         float u0 = 0.0f, v0 = 0.0f, d0 = 1e30f, u1 = 0.0f, v1 = 0.0f, d1 = 1.0f;
+        // the skew coordinate of the robot point, affine in (u, v, depth)
+        const float lam = (float)PM_PICK_SKEW_WEIGHT;
+        const float k0 = lam * dot(cf - org, w), k1 = lam * dot(t1, w), k2 = lam * dot(t2, w),
+                    k3 = 1.0f + lam * wd * dot(nref, w);
         // Branch-free selects, validity folded into the depth (+inf): kept as
         // lane masks, the candidates' 24 validity bits stayed live in SGPRs
         // across both passes and spilled ~900 of them to VGPR lanes per
@@ -859,14 +867,16 @@ struct BoxCube {
         for (int q = 0; q < 4; q++)
 #pragma unroll
             for (int k = 0; k < 3; k++) Q[q][k] = P[q][k];
+        float s0 = 1e30f;
         visit(Q, qu, qv, [&](bool ok, float u, float v, float d) {
-            const float de = ok ? d : 1e30f;
-            const bool take = de < fminf(margin, d0);
+            const float sc = (ok && d < margin) ? fmaf(k3, d, fmaf(k2, v, fmaf(k1, u, k0))) : 1e30f;
+            const bool take = sc < s0;
+            s0 = take ? sc : s0;
             u0 = take ? u : u0;
             v0 = take ? v : v0;
-            d0 = take ? de : d0;
+            d0 = take ? d : d0;
         });
-        has0 = d0 < margin;
+        has0 = s0 < 1e29f;
 #pragma unroll
         for (int q = 0; q < 4; q++)
 #pragma unroll
@@ -887,7 +897,7 @@ struct BoxCube {
         has1 = has1 && has0;
         c0 = to_world(u0, v0, d0);
         c1 = to_world(u1, v1, d1);
-        if (has1 && dot(c1.pA - org, axis) < dot(c0.pA - org, axis)) {
+        if (has1 && dot(c1.pA - org, w) < dot(c0.pA - org, w)) {
             const RCand t = c0;
             c0 = c1;
             c1 = t;
@@ -964,11 +974,14 @@ struct BoxCyl {
                 emit(ok, lB - nf * dist, lB, -nf, dist);
             }
         }
-        // 3. rim points vs the box (support_point<SHAPE_CYL, V>'s order and values)
+        // 3. rim points vs the box (support_point<SHAPE_CYL, V>'s order and
+        // values) -- only for a box with a half extent beyond the radius (the
+        // palm): a narrower box's face inside a cap is found by its vertices
         constexpr int order[PM_CYL_RIM_POINTS] = PM_CYL_RIM_ORDER;
         constexpr float c45 = 0.70710678118654752f;
+        const int nrim = (xh.x > r || xh.y > r || xh.z > r) ? num_support<SHAPE_CYL>() : 0;
 #pragma unroll 1
-        for (int V = 0; V < num_support<SHAPE_CYL>(); V++) {
+        for (int V = 0; V < nrim; V++) {
             int j = 0;
 #pragma unroll
             for (int k = 0; k < PM_CYL_RIM_POINTS; k++) j = (V % PM_CYL_RIM_POINTS) == k ? order[k] : j;
@@ -1543,7 +1556,8 @@ PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const
             const V3 xc = geo.bc[B];
             RCand c0, c1;
             int ns = 0;
-            const V3 axis = col(geo.hR, box_long_axis(B));
+            // the pick's skew direction (PM_PICK_SKEW, box frame), world
+            const V3 w = mul(geo.hR, mk((float)PM_PICK_SKEW_X, (float)PM_PICK_SKEW_Y, (float)PM_PICK_SKEW_Z));
             // a conservative bounding test first (no candidate of a pair that
             // fails it is within the margin, so the picks are unchanged): the
             // block is skipped when no lane of the wave passes it -- the palm
@@ -1561,13 +1575,14 @@ PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const
             }
             if (near) {
                 if constexpr (GROUND) {
-                    ns = pick_two([&](auto &&f) { box_ground_visit(sc, xc, geo.hR, xh, f); }, xc, axis, c0, c1);
+                    ns = pick_two<PM_BOX_GROUND_CONTACTS>([&](auto &&f) { box_ground_visit(sc, xc, geo.hR, xh, f); }, xc,
+                                                          w, c0, c1);
                 } else if constexpr (SHAPE == SHAPE_CYL) {
                     const BoxCyl bcy(sc, xc, geo.hR, xh, bd[TGT].pos, oR[TGT]);
-                    ns = pick_two([&](auto &&f) { bcy.visit(sc, f); }, xc, axis, c0, c1);
+                    ns = pick_two<PM_BOX_CONTACTS>([&](auto &&f) { bcy.visit(sc, f); }, xc, w, c0, c1);
                 } else {
                     const BoxCube bcu(xc, geo.hR, xh, bd[TGT].pos, oR[TGT], sc.half);
-                    ns = bcu.pick(xc, axis, c0, c1);
+                    ns = bcu.pick(xc, w, c0, c1);
                 }
             }
             const float mu = (float)bx.mu * (GROUND ? (float)PM_DEFAULT_FRICTION : sc.fric);

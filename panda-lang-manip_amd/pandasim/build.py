@@ -6,13 +6,15 @@ pair (step_kernels.hip: the one-lane kernel, 12 objects, and the 16/8-lane
 group kernels, 10 objects -- Stack has none) and the plugin-path substep kernel
 of each scene (sim_kernels.hip, 4 objects).
 
-The group kernels are compiled at -O1: at -O2/-O3 this compiler miscomputed
-Slide's (joint velocities off by up to 0.2 rad/s after one
-step; which kernel depended on unrelated edits and -mllvm options, and one
-experiment broke Push's 8-lane kernel the same way), while at -O1 every group
-kernel agrees with its one-lane kernel to fp32 rounding (tests/test_gpu_parity.py::
-test_group_kernels_match_one_lane) and runs as fast or faster (Push and
-PickAndPlace at 8 192 envs: 2.17 -> 2.07 ms per step).
+Every object is compiled with the same flags (-O3, no -mllvm scheduler
+options).  Round 3 built the group kernels at -O1 after an -O2/-O3 miscompute
+of Slide's; in round 4's code the -O3 group kernels are bit
+for bit the one-lane kernels (profiles/r04b_groups_o3.log), and
+tests/test_gpu_parity.py::test_group_kernels_match_one_lane requires exactly
+that, so a recurrence fails the GPU tests.  The scheduler options of round 3
+gained < 2 % in two interleaved runs (profiles/r04b_ab.log) and one of them
+(-amdgpu-use-amdgpu-trackers) made this clang crash intermittently; none is
+kept.
 
 Freshness is decided by content, not mtimes: every build writes
 ``<lib>.sha256``, the sha256 of every source and header the library is built
@@ -41,47 +43,12 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-slp-vectorize", "-f
 
 TASK_STACK = 4  # include/pandasim.h
 
-# Scheduler options of the one-lane step objects (scripts/build_variants.py
-# onelane_trk_clause, profiles/r03k_variants_sched.log): the AMDGPU register
-# pressure trackers, and memory-clause scheduling except for Stack -- every
-# task 0.3-0.9 % faster per step at 65 536 envs, Stack 2 %.  The group objects
-# take the trackers alone (groups_trk, profiles/r03k_variants_groups.log: 8-lane
-# Push/PickAndPlace at 8 192 envs 0.4 %, 16-lane at 4 096 2.7 %; memory-clause
-# scheduling was slower there).  Scheduling only: the arithmetic is unchanged.
-_SCHED = ["-mllvm", "-amdgpu-use-amdgpu-trackers"]
-_CLAUSE = ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"]
-
-
-# greedy register allocation in reverse local order: Reach 1.3 %, Slide 1.0 %,
-# Push 0.6 % faster (three interleaved runs, profiles/r03k_variants_mix.log);
-# PickAndPlace and Flip unchanged, Stack 5 % slower
-_REVERSE = ["-mllvm", "-greedy-reverse-local-assignment"]
-
-
-# Stack: the iterative minimum-register scheduler, 0.7 % faster (two
-# interleaved runs, profiles/r03k_variants_last.log).  On Reach's group
-# objects it made C2 (Reach, 4 096 envs, 16 lanes) 2.2 % faster and the 8-lane
-# Push/PickAndPlace objects 1 % slower (profiles/r03k_variants_groups2.log); not
-# adopted this round: no GPU box was free to run the group parity tests on it.
-_MINREG = ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"]
-
-
-def _one_lane_flags(task: int) -> list:
-    # no _SCHED: with the trackers this clang crashes intermittently in the
-    # scheduler's rematerialisation stage (2 of 8 parallel compiles of a group
-    # object, 7 retries for Stack's one-lane object; see compile_unit)
-    if task == TASK_STACK:
-        return _MINREG
-    return _CLAUSE + (_REVERSE if task in (0, 1, 3) else [])
-
-
 # (object name, source, defines and per-unit flags)
 UNITS = ([("pandasim", "pandasim.hip", [])]
-         + [(f"step_t{t}_c{c}", "step_kernels.hip", [f"-DPS_STEP_TASK={t}", f"-DPS_STEP_CONTROL={c}"]
-             + _one_lane_flags(t))
+         + [(f"step_t{t}_c{c}", "step_kernels.hip", [f"-DPS_STEP_TASK={t}", f"-DPS_STEP_CONTROL={c}"])
             for t in range(6) for c in range(2)]
          + [(f"step_t{t}_c{c}_groups", "step_kernels.hip",
-             [f"-DPS_STEP_TASK={t}", f"-DPS_STEP_CONTROL={c}", "-DPS_STEP_GROUPS=1", "-O1"])
+             [f"-DPS_STEP_TASK={t}", f"-DPS_STEP_CONTROL={c}", "-DPS_STEP_GROUPS=1"])
             for t in range(6) if t != TASK_STACK for c in range(2)]
          + [(f"sim_{n}_{s}", "sim_kernels.hip", [f"-DPS_SIM_NOBJ={n}", f"-DPS_SIM_SHAPE={s}"])
             for n, s in ((0, 0), (1, 0), (1, 1), (2, 0))])
