@@ -282,5 +282,6 @@ def set_link_aabb(link, lx, ly, lz):
 
 def set_state_noise(ulps: float, seed: int = 0):
     """Test hook: fp32-resolution noise of u * ulp32(x), |u| <= ulps, on every
-    state component after each substep (panda_oracle.c po_set_state_noise)."""
+    state component after each substep (panda_oracle.c po_set_state_noise);
+    ulps < 0 rounds the state to fp32 after each substep instead."""
     lib().po_set_state_noise(float(ulps), int(seed))

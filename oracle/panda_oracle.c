@@ -831,8 +831,10 @@ static void box_box_contacts(const po_config *cfg, const po_env *env, const oobj
  * PM_PICK_SKEW_WEIGHT x its coordinate along PM_PICK_SKEW (box frame) is taken
  * (the skew term decides among near-equal depths: a fingertip lying flat on
  * the table, where the deepest corner alone would be decided by rounding),
- * then -- for an object, not the ground -- the one farthest from it (0.1 mm
- * apart at least); the two are ordered along PM_PICK_SKEW, which makes the
+ * then -- for an object, not the ground -- whichever of the two candidates
+ * extreme along PM_PICK_SKEW lies farther from it along that axis (0.1 mm
+ * apart at least): one pass over the candidates, the pair spread across the
+ * contact patch; the two are ordered along PM_PICK_SKEW, which makes the
  * order (the contact's cache id) a property of the geometry.  A is the robot, B the object or ground, n points
  * from B to A. */
 typedef struct {
@@ -875,14 +877,22 @@ static int pick_contacts(const ocand *cand, int m, const double bc[3], const dou
     if (first < 0) return 0;
     out[0] = cand[first];
     if (maxn < 2) return 1;
-    int second = -1;
-    double best = 1e-8; /* (0.1 mm)^2 */
+    /* the second: the skew-extreme farther (in skew) from the first */
+    int smin = -1, smax = -1;
+    double vmin = 0.0, vmax = 0.0;
     for (int i = 0; i < m; i++) {
-        if (i == first || !(cand[i].dist < PM_CONTACT_MARGIN_ROBOT)) continue;
-        double d2 = 0.0;
-        for (int j = 0; j < 3; j++) d2 += (cand[i].pA[j] - cand[first].pA[j]) * (cand[i].pA[j] - cand[first].pA[j]);
-        if (d2 > best) { best = d2; second = i; }
+        if (!(cand[i].dist < PM_CONTACT_MARGIN_ROBOT)) continue;
+        double r[3] = {cand[i].pA[0] - bc[0], cand[i].pA[1] - bc[1], cand[i].pA[2] - bc[2]};
+        double sv = v3_dot(r, w);
+        if (smin < 0 || sv < vmin) { smin = i; vmin = sv; }
+        if (smax < 0 || sv > vmax) { smax = i; vmax = sv; }
     }
+    double rf[3] = {cand[first].pA[0] - bc[0], cand[first].pA[1] - bc[1], cand[first].pA[2] - bc[2]};
+    double s0 = v3_dot(rf, w);
+    int second = vmax - s0 >= s0 - vmin ? smax : smin;
+    double d2 = 0.0;
+    for (int j = 0; j < 3; j++) d2 += (cand[second].pA[j] - cand[first].pA[j]) * (cand[second].pA[j] - cand[first].pA[j]);
+    if (!(d2 > 1e-8)) second = -1; /* (0.1 mm)^2: the same point */
     if (second < 0) return 1;
     out[1] = cand[second];
     double r0[3], r1[3];
@@ -1451,7 +1461,8 @@ static double finger_noise(void) {
  * u uniform in [-ulps, ulps], ulp32(x) = the spacing of float32 at |x|
  * (2^(e - 24) for |x| = m 2^e, m in [0.5, 1)).  The free-run parity tests use
  * it as the yardstick of how far apart two runs that differ by the state's
- * fp32 rounding drift. */
+ * fp32 rounding drift.  ulps < 0 rounds every state component to fp32 after
+ * each substep instead (the GPU's state storage, deterministic). */
 static double state_noise_ulps = 0.0;
 void po_set_state_noise(double ulps, uint64_t seed) {
     state_noise_ulps = ulps;
@@ -1466,6 +1477,10 @@ static double unit_noise(void) {
 }
 static void ulp_noise(double *x, int n) {
     for (int k = 0; k < n; k++) {
+        if (state_noise_ulps < 0.0) { /* ulps < 0: round the state to fp32 instead */
+            x[k] = (double)(float)x[k];
+            continue;
+        }
         if (x[k] == 0.0 || !isfinite(x[k])) continue;
         int e;
         frexp(x[k], &e);

@@ -687,32 +687,40 @@ PS_D V3 colsel(const M3 &R, int c) { return c == 0 ? col(R, 0) : (c == 1 ? col(R
 template <int MAXN, class Visit>
 PS_D int pick_two(Visit &&visit, V3 org, V3 w, RCand &c0, RCand &c1) {
     const float margin = (float)PM_CONTACT_MARGIN_ROBOT;
-    bool has0 = false, has1 = false;
-    c0 = c1 = RCand{mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 1), 1.0f};
+    const RCand none{mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 1), 1.0f};
     auto sel = [](bool t, const RCand &a, const RCand &b) {
         return RCand{t ? a.pA : b.pA, t ? a.pB : b.pB, t ? a.n : b.n, t ? a.dist : b.dist};
     };
-    // validity folded into the score (see BoxCube::pick); the first pick
-    // minimises depth + PM_PICK_SKEW_WEIGHT x the coordinate along the skew
-    float s0 = 1e30f;
+    // one pass, branch-free, validity folded into the scores (see
+    // BoxCube::pick): the first pick minimises depth + PM_PICK_SKEW_WEIGHT x
+    // the skew coordinate; the candidates extreme along the skew are tracked
+    // for the second
+    RCand cmin = none, cmax = none;
+    float s0 = 1e30f, vmin = 1e30f, vmax = -1e30f;
+    c0 = none;
     visit([&](bool ok, const RCand &c) {
-        const float sc = (ok && c.dist < margin) ? fmaf((float)PM_PICK_SKEW_WEIGHT, dot(c.pA - org, w), c.dist) : 1e30f;
+        const bool valid = ok && c.dist < margin;
+        const float sv = dot(c.pA - org, w);
+        const float sc = valid ? fmaf((float)PM_PICK_SKEW_WEIGHT, sv, c.dist) : 1e30f;
         const bool take = sc < s0;
         s0 = take ? sc : s0;
         c0 = sel(take, c, c0);
+        if constexpr (MAXN >= 2) {
+            const bool tmin = valid && sv < vmin, tmax = valid && sv > vmax;
+            vmin = tmin ? sv : vmin;
+            vmax = tmax ? sv : vmax;
+            cmin = sel(tmin, c, cmin);
+            cmax = sel(tmax, c, cmax);
+        }
     });
-    has0 = s0 < 1e29f;
+    const bool has0 = s0 < 1e29f;
+    bool has1 = false;
     if constexpr (MAXN >= 2) {
-        float best = has0 ? 1e-8f : 1e30f;  // (0.1 mm)^2
-        visit([&](bool ok, const RCand &c) {
-            const V3 d = c.pA - c0.pA;
-            const float d2 = dot(d, d);
-            const bool take = (ok ? c.dist : 1e30f) < margin && d2 > best;
-            best = take ? d2 : best;
-            c1 = sel(take, c, c1);
-            has1 = has1 || take;
-        });
-        if (has1 && dot(c1.pA - org, w) < dot(c0.pA - org, w)) {
+        const float sf = dot(c0.pA - org, w);
+        c1 = sel(vmax - sf >= sf - vmin, cmax, cmin);
+        const V3 d = c1.pA - c0.pA;
+        has1 = has0 && dot(d, d) > 1e-8f;  // (0.1 mm)^2: not the same point
+        if (has1 && dot(c1.pA - org, w) < sf) {
             const RCand t = c0;
             c0 = c1;
             c1 = t;
@@ -734,15 +742,22 @@ struct BoxCube {
         int ref = 0, axn = 0;
         sep = false;
         nref = mk(0, 0, 0);
+        // the separating-axis radii from |C| = |xR^T yR| (both rotations
+        // orthonormal: a box's own axes project to its half extents), 9 dot
+        // products instead of 36
+        float C[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; i++)
+#pragma unroll
+            for (int k = 0; k < 3; k++) C[i][k] = fabsf(dot(col(xR, i), col(yR, k)));
+        const float xhv[3] = {xh.x, xh.y, xh.z}, yhv[3] = {yh.x, yh.y, yh.z};
 #pragma unroll
         for (int b = 0; b < 2; b++)
 #pragma unroll
             for (int ax = 0; ax < 3; ax++) {
                 const V3 L = col(b == 0 ? xR : yR, ax);
-                const float ra = xh.x * fabsf(dot(col(xR, 0), L)) + xh.y * fabsf(dot(col(xR, 1), L)) +
-                                 xh.z * fabsf(dot(col(xR, 2), L));
-                const float rb = yh.x * fabsf(dot(col(yR, 0), L)) + yh.y * fabsf(dot(col(yR, 1), L)) +
-                                 yh.z * fabsf(dot(col(yR, 2), L));
+                const float ra = b == 0 ? xhv[ax] : xh.x * C[0][ax] + xh.y * C[1][ax] + xh.z * C[2][ax];
+                const float rb = b == 1 ? yhv[ax] : yh.x * C[ax][0] + yh.y * C[ax][1] + yh.z * C[ax][2];
                 const float c = dot(d, L);
                 const float pen = ra + rb - fabsf(c);
                 sep = sep || pen < -(float)PM_CONTACT_MARGIN_ROBOT;
@@ -806,7 +821,7 @@ struct BoxCube {
         const float e3u = P[3][0] - P[0][0], e3v = P[3][1] - P[0][1], e3d = P[3][2] - P[0][2];
         const float pnu = e1v * e3d - e1d * e3v, pnv = e1d * e3u - e1u * e3d, pnd = e1u * e3v - e1v * e3u;
         const bool okp = pnd != 0.0f;
-        const float ipnd = okp ? 1.0f / pnd : 0.0f;
+        const float ipnd = okp ? __builtin_amdgcn_rcpf(pnd) : 0.0f;  // v_rcp_f32 (1 ulp): not an IEEE division
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const float u = cu[q] * hu, v = cv[q] * hv;
@@ -826,7 +841,7 @@ struct BoxCube {
         for (int e = 0; e < 4; e++) {
             const int e2 = (e + 1) & 3;
             const float du = P[e2][0] - P[e][0], dv = P[e2][1] - P[e][1], dd = P[e2][2] - P[e][2];
-            const float idu = du != 0.0f ? 1.0f / du : 0.0f, idv = dv != 0.0f ? 1.0f / dv : 0.0f;
+            const float idu = du != 0.0f ? __builtin_amdgcn_rcpf(du) : 0.0f, idv = dv != 0.0f ? __builtin_amdgcn_rcpf(dv) : 0.0f;
 #pragma unroll
             for (int s = 0; s < 4; s++) {
                 const bool on_u = s < 2;
@@ -850,54 +865,41 @@ struct BoxCube {
     PS_D int pick(V3 org, V3 w, RCand &c0, RCand &c1) const {
         const float margin = (float)PM_CONTACT_MARGIN_ROBOT;
         const float wd = robot_ref ? 0.0f : 1.0f;
-        bool has0 = false, has1 = false;
-        float u0 = 0.0f, v0 = 0.0f, d0 = 1e30f, u1 = 0.0f, v1 = 0.0f, d1 = 1.0f;
-        // the skew coordinate of the robot point, affine in (u, v, depth)
+        // the robot point's skew coordinate, affine in (u, v, depth)
+        const float k0 = dot(cf - org, w), k1 = dot(t1, w), k2 = dot(t2, w), k3 = wd * dot(nref, w);
         const float lam = (float)PM_PICK_SKEW_WEIGHT;
-        const float k0 = lam * dot(cf - org, w), k1 = lam * dot(t1, w), k2 = lam * dot(t2, w),
-                    k3 = 1.0f + lam * wd * dot(nref, w);
-        // Branch-free selects, validity folded into the depth (+inf): kept as
-        // lane masks, the candidates' 24 validity bits stayed live in SGPRs
-        // across both passes and spilled ~900 of them to VGPR lanes per
-        // substep.  Pass 2 recomputes the candidates from an opaque copy of
-        // the face (no common subexpressions between the passes).
-        float Q[4][3];
-        float qu = hu, qv = hv;
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-#pragma unroll
-            for (int k = 0; k < 3; k++) Q[q][k] = P[q][k];
-        float s0 = 1e30f;
-        visit(Q, qu, qv, [&](bool ok, float u, float v, float d) {
-            const float sc = (ok && d < margin) ? fmaf(k3, d, fmaf(k2, v, fmaf(k1, u, k0))) : 1e30f;
-            const bool take = sc < s0;
+        // One pass, branch-free selects, validity folded into the scores: as
+        // lane masks, the 24 candidates' validity bits stayed live in SGPRs
+        // and spilled ~900 of them to VGPR lanes per substep.
+        float s0 = 1e30f, vmin = 1e30f, vmax = -1e30f;
+        float u0 = 0.0f, v0 = 0.0f, d0 = 1.0f, un = 0.0f, vn = 0.0f, dn = 1.0f, ux = 0.0f, vx = 0.0f, dx = 1.0f;
+        visit(P, hu, hv, [&](bool ok, float u, float v, float d) {
+            const bool valid = ok && d < margin;
+            const float sv = fmaf(k3, d, fmaf(k2, v, fmaf(k1, u, k0)));
+            const float sc = valid ? fmaf(lam, sv, d) : 1e30f;
+            const bool take = sc < s0, tmin = valid && sv < vmin, tmax = valid && sv > vmax;
             s0 = take ? sc : s0;
             u0 = take ? u : u0;
             v0 = take ? v : v0;
             d0 = take ? d : d0;
+            vmin = tmin ? sv : vmin;
+            un = tmin ? u : un;
+            vn = tmin ? v : vn;
+            dn = tmin ? d : dn;
+            vmax = tmax ? sv : vmax;
+            ux = tmax ? u : ux;
+            vx = tmax ? v : vx;
+            dx = tmax ? d : dx;
         });
-        has0 = s0 < 1e29f;
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-#pragma unroll
-            for (int k = 0; k < 3; k++) asm volatile("" : "+v"(Q[q][k]));
-        asm volatile("" : "+v"(qu), "+v"(qv));
-        float best = has0 ? 1e-8f : 1e30f;  // (0.1 mm)^2
-        visit(Q, qu, qv, [&](bool ok, float u, float v, float d) {
-            const float eu = u - u0, ev = v - v0, ed = (d - d0) * wd;
-            const float e2 = eu * eu + ev * ev + ed * ed;
-            const bool take = (ok ? d : 1e30f) < margin && e2 > best;
-            best = take ? e2 : best;
-            u1 = take ? u : u1;
-            v1 = take ? v : v1;
-            d1 = take ? d : d1;
-            has1 = has1 || take;
-        });
-        has0 = has0 && !sep;
-        has1 = has1 && has0;
+        const bool has0 = s0 < 1e29f && !sep;
+        const float sf = fmaf(k3, d0, fmaf(k2, v0, fmaf(k1, u0, k0)));
+        const bool hi = vmax - sf >= sf - vmin;
+        const float u1 = hi ? ux : un, v1 = hi ? vx : vn, d1 = hi ? dx : dn;
         c0 = to_world(u0, v0, d0);
         c1 = to_world(u1, v1, d1);
-        if (has1 && dot(c1.pA - org, w) < dot(c0.pA - org, w)) {
+        const V3 dd = c1.pA - c0.pA;
+        const bool has1 = has0 && dot(dd, dd) > 1e-8f;  // (0.1 mm)^2: not the same point
+        if (has1 && (hi ? vmax : vmin) < sf) {
             const RCand t = c0;
             c0 = c1;
             c1 = t;
@@ -1562,16 +1564,20 @@ PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const
             // fails it is within the margin, so the picks are unchanged): the
             // block is skipped when no lane of the wave passes it -- the palm
             // is almost never near the table or the object
-            constexpr float rbox = (float)(bx.h[0] + bx.h[1] + bx.h[2]) + (float)PM_CONTACT_MARGIN_ROBOT;
             bool near;
             if constexpr (GROUND) {
                 const V3 ea = col(geo.hR, 0) * xh.x, eb = col(geo.hR, 1) * xh.y, ec = col(geo.hR, 2) * xh.z;
                 const float low = xc.z - (fabsf(ea.z) + fabsf(eb.z) + fabsf(ec.z));
                 near = low < (float)PM_TABLE_TOP + (float)PM_CONTACT_MARGIN_ROBOT;  // the highest ground
             } else {
-                const V3 d = xc - bd[TGT].pos;
-                const float robj = SHAPE == SHAPE_CYL ? sc.half.x + sc.half.z : sc.half.x + sc.half.y + sc.half.z;
-                near = dot(d, d) < (rbox + robj) * (rbox + robj);
+                // the object's centre against the box: its distance to the box
+                // beyond the object's bounding radius (+ margin) means no
+                // candidate can be within the margin
+                const V3 l = tmul(geo.hR, bd[TGT].pos - xc);
+                const V3 ex = mk(fmaxf(fabsf(l.x) - xh.x, 0.0f), fmaxf(fabsf(l.y) - xh.y, 0.0f), fmaxf(fabsf(l.z) - xh.z, 0.0f));
+                const float robj = (SHAPE == SHAPE_CYL ? sc.half.x + sc.half.z : sc.half.x + sc.half.y + sc.half.z) +
+                                   (float)PM_CONTACT_MARGIN_ROBOT;
+                near = dot(ex, ex) < robj * robj;
             }
             if (near) {
                 if constexpr (GROUND) {

@@ -329,6 +329,73 @@ def test_free_running_200_steps(task, control):
     assert frac >= frac_ulp - 0.02
 
 
+# Teacher forcing over the north star's horizon: every step of a 200-step run
+# (the GPU's own trajectory, random actions) is replayed by the oracle from the
+# GPU's state before it, so a systematic difference on any contact
+# configuration the run reaches shows as a step error, where a free run only
+# shows chaos.  Bounds are test_gpu_parity's per-step ones.
+LONG_TF_CASES = [("reach", "joints"), ("push", "ee"), ("push", "joints"), ("pick_and_place", "ee")]
+
+
+@pytest.mark.parametrize("task,control", LONG_TF_CASES)
+def test_teacher_forced_200_steps(task, control):
+    """64 envs x 200 steps, seed 2024 (the free runs' start): each GPU step vs
+    one oracle step from the same state.  Samples beyond the tight bounds are
+    dumped (state before and after, action, GPU observation) to
+    gpurun_out/tf200/ and listed; at most 0.1 % of env-steps may exceed them
+    (test_gpu_parity._judge: beyond the tight bounds even after the oracle's
+    own sensitivity to the state's fp32 resolution is allowed for, and not at
+    a branch the oracle cannot resolve at that resolution), none the loose ones.
+    The free-gripper PickAndPlace run holds the gripper half open (action 0), as
+    in the event-onset test, so the finger-limit bifurcations
+    stay out."""
+    from test_gpu_parity import LOOSE, _groups, _judge
+
+    B, T = 64, 200
+    env = make_env(task, control, B)
+    env.reset(seed=2024)
+    free = task == "pick_and_place"
+    if free:
+        env.sim.f[7:9, :B] = 0.02
+    cfg = oracle_config_for(env.sim.cfg)
+    groups = _groups(task, 7 if free else 6)
+    rng = np.random.default_rng(2024)
+    out = os.path.join("gpurun_out", "tf200")
+    os.makedirs(out, exist_ok=True)
+    worst = {k: 0.0 for k in groups}
+    counts = {"tight": 0, "conditioned": 0, "bif": 0, "beyond": 0}
+    beyond = []
+    for s in range(T):
+        snap = snapshot(env.sim)
+        a = rng.uniform(-1, 1, size=(B, env.action_dim)).astype(np.float32)
+        if free:
+            a[:, -1] = 0.0
+        obs, *_ = env.step(torch.from_numpy(a).cuda())
+        og = obs["observation"].cpu().numpy()
+        after = None
+        for i in range(B):
+            e = oracle_env_from(cfg, snap, i)
+            o, *_ = O.step(cfg, e, a[i])
+            cls, errs = _judge(cfg, snap, i, a[i], o, og[i], groups, task)
+            counts[cls] += 1
+            for k, err in errs.items():
+                assert err <= LOOSE[k] or cls == "bif", (k, err, s, i, cls)
+                if cls != "bif":
+                    worst[k] = max(worst[k], err)
+            if cls == "beyond":
+                beyond.append((s, i, {k: f"{v:.1e}" for k, v in errs.items()}))
+                if after is None:
+                    after = env.sim.f[:, :B].double().cpu().numpy()
+                if len(beyond) <= 40:
+                    np.savez(os.path.join(out, f"{task}_{control}_{s}_{i}.npz"), f=snap["f"][:, i],
+                             goal=snap["goal"][:, i], rng=snap["rng"][:, i], elapsed=snap["elapsed"][i], action=a[i],
+                             gpu_obs=og[i], gpu_f_after=after[:, i], oracle_obs=o)
+    print(task, control, counts, "worst (not ill-conditioned)", {k: f"{v:.2e}" for k, v in worst.items()},
+          "beyond:", beyond[:20])
+    assert counts["beyond"] <= 0.001 * B * T
+    assert counts["bif"] <= 0.02 * B * T
+
+
 def test_event_onset_parity_at_bench_config():
     """The bench workload (PandaPush-v3, 65 536 envs, ee, autoreset, seeds
     12345 + i, the bench's action stream) for 100 steps, 64 sampled envs
@@ -410,11 +477,11 @@ def test_push_and_pick_and_place_at_config_size(task):
     (lanes_per_env = 0 resolves to the 8-lane group kernel): 60 autoreset
     steps with finite, bounded observations and exact TimeLimit bookkeeping,
     then 3 steps of 64 evenly spaced envs teacher-forced against the oracle
-    at the tight bounds of test_env_step_parity_teacher_forced.  PickAndPlace
-    (free gripper) holds the samples the oracle itself cannot resolve at fp32
-    resolution (finger-limit branches: _ill_conditioned) to the loose bounds
-    instead, at most 8 % of them."""
-    from test_gpu_parity import FREE_GRIPPER, LOOSE, TOL, _groups, _ill_conditioned, _within
+    at the tight bounds of test_env_step_parity_teacher_forced (test_gpu_parity
+    ._judge): samples the oracle itself cannot resolve at fp32 resolution
+    (finger- and joint-limit branches) are held to the loose bounds instead,
+    at most 8 % of them."""
+    from test_gpu_parity import FREE_GRIPPER, LOOSE, _groups, _judge
 
     from pandasim.envs import PandaVecEnv
 
@@ -432,15 +499,16 @@ def test_push_and_pick_and_place_at_config_size(task):
         assert torch.equal(tr, steps_in_episode == env.max_episode_steps)
         steps_in_episode[te | tr] = 0
         assert torch.isfinite(obs["observation"]).all()
-        assert (obs["observation"].abs() < 100).all()
+        # a gripper strike can spin a cube to ~100 rad/s (the fp64 oracle does
+        # too: 116 rad/s in 8 192 PickAndPlace envs); a blow-up is far beyond
+        assert (obs["observation"].abs() < 1000).all()
     assert torch.equal(env.sim.elapsed[:B].long(), steps_in_episode)
     env.autoreset = False
     cfg = oracle_config_for(env.sim.cfg)
     groups = _groups(task, 7 if task in FREE_GRIPPER else 6)
-    tol = TOL[task]
     sample = np.linspace(0, B - 1, 64).astype(int)
     worst = {k: 0.0 for k in groups}
-    n_bif = 0
+    counts = {"tight": 0, "conditioned": 0, "bif": 0, "beyond": 0}
     for s in range(3):
         snap = snapshot(env.sim)
         a = torch.rand(B, env.action_dim, device="cuda", generator=g) * 2 - 1
@@ -450,16 +518,15 @@ def test_push_and_pick_and_place_at_config_size(task):
         for i in sample:
             o, ag, dg, rr, t_e, t_r = O.step(cfg, oracle_env_from(cfg, snap, i), a[i])
             assert t_r == bool(tr[i]), (s, i)
-            bif = task in FREE_GRIPPER and _ill_conditioned(cfg, snap, i, a[i], o, groups, tol)
-            n_bif += bif
-            for k, idx in groups.items():
-                err = float(np.abs(og[i, idx] - o[idx]).max())
-                assert _within(err, o[idx], k, LOOSE if bif else tol), (task, s, i, k, err, bif)
-                if not bif:
+            cls, errs = _judge(cfg, snap, i, a[i], o, og[i], groups, task)
+            counts[cls] += 1
+            assert cls != "beyond", (task, s, i, errs)
+            for k, err in errs.items():
+                assert cls != "bif" or err <= LOOSE[k], (task, s, i, k, err)
+                if cls != "bif":
                     worst[k] = max(worst[k], err)
-    print(task, f"{B} envs, 8 lanes:", {k: f"{v:.1e}" for k, v in worst.items()},
-          f"ill-conditioned {n_bif}/{3 * len(sample)}")
-    assert n_bif <= 0.08 * 3 * len(sample)
+    print(task, f"{B} envs, 8 lanes:", {k: f"{v:.1e}" for k, v in worst.items()}, counts)
+    assert counts["bif"] <= 0.08 * 3 * len(sample)
 
 
 def test_bench_config_after_60_steps():
