@@ -19,11 +19,12 @@
 // each wave accumulates s_memtime deltas per phase and lane 0 adds them to
 // ps_phase_cycles at the end of the kernel.  Compiled out of the product.
 #define PS_NUM_PHASES 8
-#define PS_NUM_PROF_SLOTS 20  // phases + PGS counters (lane iterations, wave iterations, substeps, robot-contact slots run,
+#define PS_NUM_PROF_SLOTS 24  // phases + PGS counters (lane iterations, wave iterations, substeps, robot-contact slots run,
                               // the wave's open row gates: pair slots, ground slots, robot slots, joint limits;
                               // 16-18: sub-phases of rows+contacts -- 16 joint rows, 17 gripper contact
                               // candidates, 18 object ground/pair contacts -- the rest of it, the gripper
-                              // rows, stays in 3)
+                              // rows, stays in 3; 20-23: gripper candidate blocks -- lanes passing the
+                              // bounding test and blocks run, box-object then box-ground)
 #ifdef PS_PROFILE_PHASES
 struct PhaseTimer {
     uint64_t last, acc[PS_NUM_PROF_SLOTS];

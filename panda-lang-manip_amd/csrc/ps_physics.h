@@ -1540,62 +1540,191 @@ struct RobotCand {
 };
 static_assert(RobotCand::OFFSET + NR * RobotCand::FLOATS <= NR * 27, "candidate records inside the M^-1 J^T area");
 
-template <int NOBJ, int SHAPE>
-PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const M3 *oR, const MJStore &lds) {
+// position of the j-th (from 0) set bit of m (j < popcount(m)), branch-free
+PS_D int nth_set_bit(uint64_t m, int j) {
+    int pos = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const uint64_t low = m & ((1ull << w) - 1ull);
+        const int c = __builtin_popcountll(low);
+        const bool up = j >= c;
+        j = up ? j - c : j;
+        pos += up ? w : 0;
+        m = up ? (m >> w) : low;
+    }
+    return pos;
+}
+
+// Candidate work lists.  The bounding tests pass for few lanes of a wave (Push,
+// 65 536 envs: 2.2 lanes of 64 per box-object test that passes anywhere, 14 per
+// box-ground one; profiles/r04f_phase_push.log), and run per lane the pair's
+// candidate block cost the whole wave a block per box.  Instead the (env, box)
+// pairs that pass are numbered box-major across the wave (ballot + popcount),
+// the owners park their geometry in their own LDS column, and active lane k
+// evaluates pair k of the round -- one block per round for the wave, not one per
+// box -- and leaves its picks in its column, which the owners read back in box
+// order (the slot order of the per-lane version: the same values, bit for bit).
+// Scratch: floats [0, 51) of each column, below the RobotCand records.
+constexpr int CW_IN = 0;    // owner: hR (9), box centres (3 x 3), object position (3), rotation (9)
+constexpr int CW_OUT = 30;  // worker: pick 0 (pA, pB, n, dist), pick 1, count
+static_assert(CW_OUT + 21 <= RobotCand::OFFSET, "work-list scratch below the candidate records");
+
+template <int NOBJ, int SHAPE, int G>
+PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const M3 *oR, const MJStore &lds PS_PROF_PARAM) {
     int nr = 0;
     auto offer = [&](const RobotCand &c) {
         c.store(lds, nr);
         nr++;
     };
     constexpr SphereDef ws = wrist_def();
+    constexpr int NBX = PM_NUM_BOXES;
+    const uint32_t lane = __lane_id();
+    const uint64_t act = __ballot(true);  // G == 1: lanes past the batch end have returned
+    const int nact = __builtin_popcountll(act);
+    const int rank = __builtin_popcountll(act & ((1ull << lane) - 1ull));
+    // G > 1: every lane of a group holds the same env; its first lane owns the pairs
+    const uint32_t leader = lane & ~(uint32_t)(G - 1);
+    const uint64_t below = (1ull << leader) - 1ull;
+    lds_float *const col0 = lds.base - lane;  // column 0 of the wave's LDS block
+    auto at = [&](int k, int c) -> lds_float & { return col0[k * lds.stride + c]; };
     static_for<0, NOBJ + 1>([&](auto TT) {
         constexpr int TGT = decltype(TT)::value == NOBJ ? 2 : decltype(TT)::value;
         constexpr bool GROUND = TGT == 2;
-        static_for<0, PM_NUM_BOXES>([&](auto BB) {
+        // a conservative bounding test per box first (no candidate of a pair
+        // that fails it is within the margin, so the picks are unchanged)
+        bool nearb[NBX];
+        uint64_t m[NBX];
+        int pre[NBX + 1];
+        pre[0] = 0;
+        static_for<0, NBX>([&](auto BB) {
             constexpr int B = decltype(BB)::value;
             constexpr BoxDef bx = box_def(B);
             const V3 xh = mk((float)bx.h[0], (float)bx.h[1], (float)bx.h[2]);
             const V3 xc = geo.bc[B];
-            RCand c0, c1;
-            int ns = 0;
-            // the pick's skew direction (PM_PICK_SKEW, box frame), world
-            const V3 w = mul(geo.hR, mk((float)PM_PICK_SKEW_X, (float)PM_PICK_SKEW_Y, (float)PM_PICK_SKEW_Z));
-            // a conservative bounding test first (no candidate of a pair that
-            // fails it is within the margin, so the picks are unchanged): the
-            // block is skipped when no lane of the wave passes it -- the palm
-            // is almost never near the table or the object
-            bool near;
             if constexpr (GROUND) {
                 const V3 ea = col(geo.hR, 0) * xh.x, eb = col(geo.hR, 1) * xh.y, ec = col(geo.hR, 2) * xh.z;
                 const float low = xc.z - (fabsf(ea.z) + fabsf(eb.z) + fabsf(ec.z));
-                near = low < (float)PM_TABLE_TOP + (float)PM_CONTACT_MARGIN_ROBOT;  // the highest ground
+                nearb[B] = low < (float)PM_TABLE_TOP + (float)PM_CONTACT_MARGIN_ROBOT;  // the highest ground
             } else {
                 // the object's centre against the box: its distance to the box
                 // beyond the object's bounding radius (+ margin) means no
-                // candidate can be within the margin
+                // candidate can be within the margin (a sphere around the
+                // object: |half| bounds a box and, with half = (r, r, h), a
+                // cylinder)
                 const V3 l = tmul(geo.hR, bd[TGT].pos - xc);
                 const V3 ex = mk(fmaxf(fabsf(l.x) - xh.x, 0.0f), fmaxf(fabsf(l.y) - xh.y, 0.0f), fmaxf(fabsf(l.z) - xh.z, 0.0f));
-                const float robj = (SHAPE == SHAPE_CYL ? sc.half.x + sc.half.z : sc.half.x + sc.half.y + sc.half.z) +
-                                   (float)PM_CONTACT_MARGIN_ROBOT;
-                near = dot(ex, ex) < robj * robj;
+                const float robj = sqrtf(dot(sc.half, sc.half)) + (float)PM_CONTACT_MARGIN_ROBOT;
+                nearb[B] = dot(ex, ex) < robj * robj;
             }
-            if (near) {
-                if constexpr (GROUND) {
-                    ns = pick_two<PM_BOX_GROUND_CONTACTS>([&](auto &&f) { box_ground_visit(sc, xc, geo.hR, xh, f); }, xc,
-                                                          w, c0, c1);
-                } else if constexpr (SHAPE == SHAPE_CYL) {
-                    const BoxCyl bcy(sc, xc, geo.hR, xh, bd[TGT].pos, oR[TGT]);
-                    ns = pick_two<PM_BOX_CONTACTS>([&](auto &&f) { bcy.visit(sc, f); }, xc, w, c0, c1);
-                } else {
-                    const BoxCube bcu(xc, geo.hR, xh, bd[TGT].pos, oR[TGT], sc.half);
-                    ns = bcu.pick(xc, w, c0, c1);
-                }
-            }
-            const float mu = (float)bx.mu * (GROUND ? (float)PM_DEFAULT_FRICTION : sc.fric);
-            const int obj = GROUND ? -1 : TGT;
-            if (nr < NR && ns >= 1) offer(RobotCand{c0.pA, c0.pB, c0.n, c0.dist, mu, bx.link, obj, 1 + (B * 3 + TGT) * 2});
-            if (nr < NR && ns >= 2) offer(RobotCand{c1.pA, c1.pB, c1.n, c1.dist, mu, bx.link, obj, 2 + (B * 3 + TGT) * 2});
+            m[B] = __ballot(nearb[B] && lane == leader);
+            pre[B + 1] = pre[B] + __builtin_popcountll(m[B]);
+#ifdef PS_PROFILE_PHASES
+            pt.acc[GROUND ? 22 : 20] += __builtin_popcountll(m[B]);
+            pt.acc[GROUND ? 23 : 21] += m[B] != 0;
+#endif
         });
+        const int total = pre[NBX];
+        if (total > 0) {
+            // the owner's geometry, in its own column
+#pragma unroll
+            for (int k = 0; k < 9; k++) lds.base[(CW_IN + k) * lds.stride] = geo.hR.m[k];
+#pragma unroll
+            for (int b = 0; b < NBX; b++) {
+                lds.base[(CW_IN + 9 + 3 * b) * lds.stride] = geo.bc[b].x;
+                lds.base[(CW_IN + 10 + 3 * b) * lds.stride] = geo.bc[b].y;
+                lds.base[(CW_IN + 11 + 3 * b) * lds.stride] = geo.bc[b].z;
+            }
+            if constexpr (!GROUND) {
+                lds.base[(CW_IN + 18) * lds.stride] = bd[TGT].pos.x;
+                lds.base[(CW_IN + 19) * lds.stride] = bd[TGT].pos.y;
+                lds.base[(CW_IN + 20) * lds.stride] = bd[TGT].pos.z;
+#pragma unroll
+                for (int k = 0; k < 9; k++) lds.base[(CW_IN + 21 + k) * lds.stride] = oR[TGT].m[k];
+            }
+            for (int r = 0; r < total; r += nact) {
+                __syncthreads();
+                const int k = r + rank;
+                if (k < total) {
+                    int B = 0;
+#pragma unroll
+                    for (int b = 1; b < NBX; b++) B = k >= pre[b] ? b : B;
+                    uint64_t mb = m[0];
+                    int pb = 0;
+#pragma unroll
+                    for (int b = 1; b < NBX; b++) {
+                        mb = B == b ? m[b] : mb;
+                        pb = B == b ? pre[b] : pb;
+                    }
+                    const int own = nth_set_bit(mb, k - pb);
+                    M3 hR;
+#pragma unroll
+                    for (int q = 0; q < 9; q++) hR.m[q] = at(CW_IN + q, own);
+                    // (selected per component: selects of whole vectors went
+                    // through a stack array)
+                    const int cb = CW_IN + 9 + 3 * B;
+                    const V3 xc = mk(at(cb, own), at(cb + 1, own), at(cb + 2, own));
+                    float hx = (float)box_def(0).h[0], hy = (float)box_def(0).h[1], hz = (float)box_def(0).h[2];
+#pragma unroll
+                    for (int b = 1; b < NBX; b++) {
+                        hx = B == b ? (float)box_def(b).h[0] : hx;
+                        hy = B == b ? (float)box_def(b).h[1] : hy;
+                        hz = B == b ? (float)box_def(b).h[2] : hz;
+                    }
+                    const V3 xh = mk(hx, hy, hz);
+                    // the pick's skew direction (PM_PICK_SKEW, box frame), world
+                    const V3 w = mul(hR, mk((float)PM_PICK_SKEW_X, (float)PM_PICK_SKEW_Y, (float)PM_PICK_SKEW_Z));
+                    RCand c0, c1;
+                    int ns;
+                    if constexpr (GROUND) {
+                        ns = pick_two<PM_BOX_GROUND_CONTACTS>([&](auto &&f) { box_ground_visit(sc, xc, hR, xh, f); }, xc, w,
+                                                              c0, c1);
+                    } else {
+                        const V3 yc = mk(at(CW_IN + 18, own), at(CW_IN + 19, own), at(CW_IN + 20, own));
+                        M3 yR;
+#pragma unroll
+                        for (int q = 0; q < 9; q++) yR.m[q] = at(CW_IN + 21 + q, own);
+                        if constexpr (SHAPE == SHAPE_CYL) {
+                            const BoxCyl bcy(sc, xc, hR, xh, yc, yR);
+                            ns = pick_two<PM_BOX_CONTACTS>([&](auto &&f) { bcy.visit(sc, f); }, xc, w, c0, c1);
+                        } else {
+                            const BoxCube bcu(xc, hR, xh, yc, yR, sc.half);
+                            ns = bcu.pick(xc, w, c0, c1);
+                        }
+                    }
+                    const float out[21] = {c0.pA.x, c0.pA.y, c0.pA.z, c0.pB.x, c0.pB.y, c0.pB.z, c0.n.x, c0.n.y, c0.n.z,
+                                           c0.dist, c1.pA.x, c1.pA.y, c1.pA.z, c1.pB.x, c1.pB.y, c1.pB.z, c1.n.x, c1.n.y,
+                                           c1.n.z, c1.dist, (float)ns};
+                    const int nout = GROUND && PM_BOX_GROUND_CONTACTS < 2 ? 10 : 20;
+#pragma unroll
+                    for (int q = 0; q < 20; q++)
+                        if (q < nout) lds.base[(CW_OUT + q) * lds.stride] = out[q];
+                    lds.base[(CW_OUT + 20) * lds.stride] = out[20];
+                }
+                __syncthreads();
+                // the owners take their pairs of this round, in box order
+                static_for<0, NBX>([&](auto BB) {
+                    constexpr int B = decltype(BB)::value;
+                    constexpr BoxDef bx = box_def(B);
+                    const int idx = pre[B] + __builtin_popcountll(m[B] & below) - r;
+                    if (nearb[B] && idx >= 0 && idx < nact) {
+                        const int wl = nth_set_bit(act, idx);
+                        const int ns = (int)at(CW_OUT + 20, wl);
+                        const float mu = (float)bx.mu * (GROUND ? (float)PM_DEFAULT_FRICTION : sc.fric);
+                        const int obj = GROUND ? -1 : TGT;
+#pragma unroll
+                        for (int c = 0; c < 2; c++) {
+                            if (nr < NR && ns > c) {
+                                const int o = CW_OUT + 10 * c;
+                                offer(RobotCand{mk(at(o, wl), at(o + 1, wl), at(o + 2, wl)),
+                                                mk(at(o + 3, wl), at(o + 4, wl), at(o + 5, wl)),
+                                                mk(at(o + 6, wl), at(o + 7, wl), at(o + 8, wl)), at(o + 9, wl), mu, bx.link,
+                                                obj, 1 + c + (B * 3 + TGT) * 2});
+                            }
+                        }
+                    }
+                });
+            }
+        }
         constexpr int WID = 1 + (PM_NUM_BOXES * 3 + TGT) * 2;
         if constexpr (GROUND) {
             float top;
@@ -1671,7 +1800,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         M3 oR[NB];
 #pragma unroll
         for (int b = 0; b < NB; b++) oR[b] = NOBJ > 0 ? quat_to_mat(bd[b].quat) : M3{{1, 0, 0, 0, 1, 0, 0, 0, 1}};
-        nr = robot_candidates<NOBJ, SHAPE>(sc, geo, bd, oR, lds);
+        nr = robot_candidates<NOBJ, SHAPE, G>(sc, geo, bd, oR, lds PS_PROF_ARG);
     }
     PS_PHASE(17);
     __builtin_amdgcn_sched_barrier(0);

@@ -28,7 +28,7 @@ def main():
     env.reset(seed=12345)
     lib = L.lib()
     lib.ps_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int]
-    buf = (C.c_ulonglong * 20)()
+    buf = (C.c_ulonglong * 24)()
     g = torch.Generator(device="cuda")
     g.manual_seed(0xC0FFEE)
     for k in range(5):
@@ -55,6 +55,10 @@ def main():
           f"max robot contacts per wave {buf[11] / subs:.2f}")
     print(f"  open row gates per wave-substep: pair slots {buf[12] / subs:.2f}, ground slots {buf[13] / subs:.2f}, "
           f"robot slots {buf[14] / subs:.2f}, joint limits {buf[15] / subs:.2f}")
+    if buf[21] or buf[23]:
+        print(f"  gripper candidate blocks per wave-substep: box-object {buf[21] / subs:.2f} run "
+              f"({buf[20] / max(buf[21], 1):.1f} lanes of 64 near when run), box-ground {buf[23] / subs:.2f} run "
+              f"({buf[22] / max(buf[23], 1):.1f} lanes near when run)")
 
 
 if __name__ == "__main__":
