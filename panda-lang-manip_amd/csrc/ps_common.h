@@ -26,8 +26,10 @@
                               // rows, stays in 3; 20-23: gripper candidate blocks -- lanes passing the
                               // bounding test and blocks run, box-object then box-ground)
 #ifdef PS_PROFILE_PHASES
+// (32-bit: one kernel's wave-cycles per phase fit, and 64-bit accumulators
+// cost the instrumented kernel another PS_NUM_PROF_SLOTS VGPRs at 512)
 struct PhaseTimer {
-    uint64_t last, acc[PS_NUM_PROF_SLOTS];
+    uint32_t last, acc[PS_NUM_PROF_SLOTS];
 };
 #define PS_PROF_PARAM , PhaseTimer &pt
 #define PS_PROF_ARG , pt
@@ -35,7 +37,7 @@ struct PhaseTimer {
 #define PS_PROF_COUNT_ARG , prof_it
 #define PS_PHASE(k)                                        \
     do {                                                   \
-        uint64_t ps_t_now = __builtin_amdgcn_s_memtime();  \
+        uint32_t ps_t_now = (uint32_t)__builtin_amdgcn_s_memtime(); \
         pt.acc[k] += ps_t_now - pt.last;                   \
         pt.last = ps_t_now;                                \
     } while (0)

@@ -630,7 +630,7 @@ __global__ __launch_bounds__(kBlock, PS_STEP_MIN_WAVES) void k_step(KParams P, c
     const StateView &s = P.s;
 #ifdef PS_PROFILE_PHASES
     PhaseTimer pt;
-    pt.last = __builtin_amdgcn_s_memtime();
+    pt.last = (uint32_t)__builtin_amdgcn_s_memtime();
     for (int k = 0; k < PS_NUM_PROF_SLOTS; k++) pt.acc[k] = 0;
 #endif
     float q[9], qd[9];
@@ -765,7 +765,7 @@ __global__ __launch_bounds__(kBlock) void k_sim_step(KParams P, int n_substeps) 
     }
 #ifdef PS_PROFILE_PHASES
     PhaseTimer pt;
-    pt.last = __builtin_amdgcn_s_memtime();
+    pt.last = (uint32_t)__builtin_amdgcn_s_memtime();
     for (int k = 0; k < PS_NUM_PROF_SLOTS; k++) pt.acc[k] = 0;
 #endif
     run_substeps<NOBJ, SHAPE, false>(P, i, n_substeps, q, qd, bd, lds, true, nullptr PS_PROF_ARG);
