@@ -246,7 +246,9 @@ PS_D void bias_forces(const float q[9], const float qd[9], float h[9]) {
 
 // M = L L^T, then M^-1 (packed symmetric) = L^-T L^-1
 PS_D void spd_inverse(float M[45]) {
-    float L[45];
+    // Cholesky with one reciprocal per column: the 36 off-diagonal divisions
+    // are products with it (an IEEE division is ~10 VALU instructions)
+    float L[45], invd[9];
 #pragma unroll
     for (int i = 0; i < 9; i++) {
 #pragma unroll
@@ -254,15 +256,19 @@ PS_D void spd_inverse(float M[45]) {
             float s = M[sidx(i, j)];
 #pragma unroll
             for (int q = 0; q < j; q++) s -= L[sidx(i, q)] * L[sidx(j, q)];
-            if (i == j) L[sidx(i, i)] = sqrtf(s);
-            else L[sidx(i, j)] = s / L[sidx(j, j)];
+            if (i == j) {
+                L[sidx(i, i)] = sqrtf(s);
+                invd[i] = 1.0f / L[sidx(i, i)];
+            } else {
+                L[sidx(i, j)] = s * invd[j];
+            }
         }
     }
     // invert L in place (lower triangular)
     float Li[45];
 #pragma unroll
     for (int i = 0; i < 9; i++) {
-        float inv = 1.0f / L[sidx(i, i)];
+        const float inv = invd[i];
         Li[sidx(i, i)] = inv;
 #pragma unroll
         for (int j = 0; j < i; j++) {
