@@ -642,3 +642,37 @@ def test_nonfinite_guard_flags_and_resets():
     env.set_nonfinite_guard(False)
     obs, r, te, tr, info = env.step(a[2])
     assert "nonfinite" not in info
+
+
+@pytest.mark.parametrize("task,lanes", [("push", 1), ("slide", 1), ("stack", 1), ("pick_and_place", 1),
+                                        ("push", 8), ("pick_and_place", 16)])
+def test_gripper_work_lists_are_lane_independent(task, lanes):
+    """The gripper candidates are evaluated on whichever lane of the wave the
+    work list assigns (ps_physics.h robot_candidates): an env's step must not
+    depend on which other envs share its wave, nor on a partial last wave
+    (one-lane kernels: lanes past the batch end have returned).  A scripted
+    push into the object (contact-rich) from the same seeds, in batches of
+    128, 100 (a partial second wave) and 36 (the partial wave alone): every
+    env's state is equal bit for bit across the three."""
+    from pandasim.envs import PandaVecEnv
+
+    seeds = (777 + np.arange(128)).astype(np.uint64)
+    body = "object1" if task == "stack" else "object"
+    runs = {}
+    for lo, hi in ((0, 128), (0, 100), (64, 100)):
+        B = hi - lo
+        env = PandaVecEnv(task, "sparse", "ee", B, "cuda", lanes_per_env=lanes)
+        assert env.lanes_per_env == lanes
+        env.autoreset = False
+        env.reset(seed=seeds[lo:hi])
+        policy = _push_policy(env, body)
+        contacts = 0
+        for s in range(14):
+            env.step(torch.from_numpy(policy(s)).cuda())
+            ids = env.sim.f[WR_ROW + 4, :B].cpu().numpy()
+            contacts += int((ids != 0).sum())
+        assert contacts > 0  # the gripper rows are exercised
+        runs[(lo, hi)] = env.sim.f[:, :B].cpu().numpy()
+    full = runs[(0, 128)]
+    assert np.array_equal(runs[(0, 100)], full[:, :100])
+    assert np.array_equal(runs[(64, 100)], full[:, 64:100])
