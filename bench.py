@@ -128,6 +128,19 @@ def oracle_work_counts(O, cfg, n_env: int = 64, steps: int = 60) -> dict:
     return st.as_dict()
 
 
+WORK_COUNTS = "profiles/oracle_work_counts.json"
+
+
+def committed_work_counts(task: str):
+    """oracle_work_counts() of `task` as committed by scripts/oracle_work_counts.py
+    (a data file: nothing under oracle/ runs), or None."""
+    try:
+        with open(os.path.join(ROOT, WORK_COUNTS)) as f:
+            return json.load(f).get(task)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -404,9 +417,18 @@ def main():
                            "mean_last_return": round(float(ep[0][done].mean()), 4) if done.any() else None,
                            "last_success_rate": round(float(ep[1][done].mean()), 4) if done.any() else None,
                            "gathered_envs": int(ep.shape[1])}
+        work = None
         if world == 1 and not args.no_cpu_baseline:
             work, out["cpu_baseline"] = cpu_baseline(spec["task"], args.cpu_seconds)
+        else:
+            # N > 1 (the CPU baseline is rank 0's at N = 1 only) or no CPU leg:
+            # the FLOP roofline from the committed work counts of the same
+            # oracle sample (scripts/oracle_work_counts.py)
+            work = committed_work_counts(spec["task"])
+        if work is not None:
             out["roofline"]["fp32"] = fp32_roofline(work, env.sim.cfg.n_objects, value / world)
+            if world > 1 or args.no_cpu_baseline:
+                out["roofline"]["fp32"]["work_source"] = WORK_COUNTS
             ex = out["roofline"].get("fp32_executed")
             if ex:
                 # executed (PMC) over algorithmic FLOPs per launch: the share of

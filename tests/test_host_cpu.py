@@ -315,3 +315,18 @@ def test_bench_pmc_fields_are_tied_to_the_binary(tmp_path):
     lib.write_bytes(b"\x7fELF rebuilt")  # the library changed after the profile
     e, info = bench.pmc_entry("W", str(lib), str(pmc))
     assert e is None and info["status"] == "stale" and info["measured_on"] == good
+
+
+def test_bench_fp32_roofline_without_the_cpu_leg():
+    """N > 1 (and --no-cpu-baseline) lines carry roofline.fp32 from the
+    committed oracle work counts (profiles/oracle_work_counts.json, written by
+    scripts/oracle_work_counts.py): present for every task, and the FLOPs per
+    env-step they give match the ones the bench's own CPU leg measured."""
+    import bench
+
+    for task in ("reach", "push", "pick_and_place", "slide", "stack", "flip"):
+        w = bench.committed_work_counts(task)
+        assert w and w["substeps"] > 0 and w["pgs_iterations"] > 0, task
+    r = bench.fp32_roofline(bench.committed_work_counts("push"), 1, 2.1e7)
+    assert 5.0e5 < r["flops_per_env_step"] < 6.5e5
+    assert bench.committed_work_counts("no such task") is None
