@@ -23,8 +23,9 @@
                               // the wave's open row gates: pair slots, ground slots, robot slots, joint limits;
                               // 16-18: sub-phases of rows+contacts -- 16 joint rows, 17 gripper contact
                               // candidates, 18 object ground/pair contacts -- the rest of it, the gripper
-                              // rows, stays in 3; 20-23: gripper candidate blocks -- lanes passing the
-                              // bounding test and blocks run, box-object then box-ground)
+                              // rows, stays in 3; 20-23: gripper bounding tests -- (env, box) pairs
+                              // passing them and boxes passing for some env of the wave, box-object
+                              // then box-ground)
 #ifdef PS_PROFILE_PHASES
 // (32-bit: one kernel's wave-cycles per phase fit, and 64-bit accumulators
 // cost the instrumented kernel another PS_NUM_PROF_SLOTS VGPRs at 512)

@@ -56,9 +56,9 @@ def main():
     print(f"  open row gates per wave-substep: pair slots {buf[12] / subs:.2f}, ground slots {buf[13] / subs:.2f}, "
           f"robot slots {buf[14] / subs:.2f}, joint limits {buf[15] / subs:.2f}")
     if buf[21] or buf[23]:
-        print(f"  gripper candidate blocks per wave-substep: box-object {buf[21] / subs:.2f} run "
-              f"({buf[20] / max(buf[21], 1):.1f} lanes of 64 near when run), box-ground {buf[23] / subs:.2f} run "
-              f"({buf[22] / max(buf[23], 1):.1f} lanes near when run)")
+        print(f"  gripper bounding tests per wave-substep: box-object passed for {buf[21] / subs:.2f} boxes "
+              f"({buf[20] / max(buf[21], 1):.1f} envs of the wave each), box-ground for {buf[23] / subs:.2f} "
+              f"({buf[22] / max(buf[23], 1):.1f} envs each); the work lists evaluate them in one round per pass")
 
 
 if __name__ == "__main__":
