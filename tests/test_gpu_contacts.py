@@ -379,7 +379,9 @@ def test_free_running_200_steps(task, control):
 # GPU's state before it, so a systematic difference on any contact
 # configuration the run reaches shows as a step error, where a free run only
 # shows chaos.  Bounds are test_gpu_parity's per-step ones.
-LONG_TF_CASES = [("reach", "joints"), ("push", "ee"), ("push", "joints"), ("pick_and_place", "ee")]
+LONG_TF_CASES = [("reach", "joints"), ("push", "ee"), ("push", "joints"), ("pick_and_place", "ee"), ("slide", "ee"),
+                 ("stack", "ee"), ("flip", "ee")]
+FREE_GRIPPER_TASKS = ("pick_and_place", "stack", "flip")
 
 
 @pytest.mark.parametrize("task,control", LONG_TF_CASES)
@@ -391,15 +393,15 @@ def test_teacher_forced_200_steps(task, control):
     (test_gpu_parity._judge: beyond the tight bounds even after the oracle's
     own sensitivity to the state's fp32 resolution is allowed for, and not at
     a branch the oracle cannot resolve at that resolution), none the loose ones.
-    The free-gripper PickAndPlace run holds the gripper half open (action 0), as
-    in the event-onset test, so the finger-limit bifurcations
-    stay out."""
+    The free-gripper runs (PickAndPlace, Stack, Flip) hold the gripper half
+    open (action 0), as in the event-onset test, so the finger-limit
+    bifurcations stay out."""
     from test_gpu_parity import LOOSE, _groups, _judge
 
     B, T = 64, 200
     env = make_env(task, control, B)
     env.reset(seed=2024)
-    free = task == "pick_and_place"
+    free = task in FREE_GRIPPER_TASKS
     if free:
         env.sim.f[7:9, :B] = 0.02
     cfg = oracle_config_for(env.sim.cfg)
