@@ -120,7 +120,10 @@ PS_D Comp combine(const Comp &a, const Comp &b) {
     c.m = a.m + b.m;
     float inv = 1.0f / c.m;
     c.h = (a.h * a.m + b.h * b.m) * inv;
-    c.I = a.I + b.I + shift(a.m, a.h - c.h) + shift(b.m, b.h - c.h);
+    // the two parallel-axis terms about the joint COM are one with the
+    // reduced mass m_a m_b / (m_a + m_b) and d = h_a - h_b (masses are
+    // compile-time constants, so is the factor)
+    c.I = a.I + b.I + shift(a.m * b.m * inv, a.h - b.h);
     return c;
 }
 
@@ -345,8 +348,9 @@ PS_D void inverse_kinematics(const float q_start[9], V3 target, Q4 orn, float q_
             for (int b = 0; b <= a; b++)
                 U[a * (a + 1) / 2 + b] = dot(Jv[a], Jv[b]) + dot(Jw[a], Jw[b]) + (a == b ? (float)PM_IK_DAMPING : 0.0f);
         }
-        // Cholesky solve
-        float Lc[N * (N + 1) / 2];
+        // Cholesky solve, one reciprocal per pivot (the divisions by it are
+        // products: an IEEE division is ~10 VALU instructions)
+        float Lc[N * (N + 1) / 2], il[N];
 #pragma unroll
         for (int i = 0; i < N; i++)
 #pragma unroll
@@ -354,8 +358,12 @@ PS_D void inverse_kinematics(const float q_start[9], V3 target, Q4 orn, float q_
                 float s = U[i * (i + 1) / 2 + j];
 #pragma unroll
                 for (int t = 0; t < j; t++) s -= Lc[i * (i + 1) / 2 + t] * Lc[j * (j + 1) / 2 + t];
-                if (i == j) Lc[i * (i + 1) / 2 + i] = sqrtf(s);
-                else Lc[i * (i + 1) / 2 + j] = s / Lc[j * (j + 1) / 2 + j];
+                if (i == j) {
+                    Lc[i * (i + 1) / 2 + i] = sqrtf(s);
+                    il[i] = 1.0f / Lc[i * (i + 1) / 2 + i];
+                } else {
+                    Lc[i * (i + 1) / 2 + j] = s * il[j];
+                }
             }
         float y[N], x[N];
 #pragma unroll
@@ -363,14 +371,14 @@ PS_D void inverse_kinematics(const float q_start[9], V3 target, Q4 orn, float q_
             float s = g[i];
 #pragma unroll
             for (int t = 0; t < i; t++) s -= Lc[i * (i + 1) / 2 + t] * y[t];
-            y[i] = s / Lc[i * (i + 1) / 2 + i];
+            y[i] = s * il[i];
         }
 #pragma unroll
         for (int i = N - 1; i >= 0; i--) {
             float s = y[i];
 #pragma unroll
             for (int t = i + 1; t < N; t++) s -= Lc[t * (t + 1) / 2 + i] * x[t];
-            x[i] = s / Lc[i * (i + 1) / 2 + i];
+            x[i] = s * il[i];
         }
         float mx = 0.0f;
 #pragma unroll
@@ -1036,17 +1044,21 @@ PS_D void box_ground_visit(const Scene &sc, V3 xc, const M3 &xR, V3 xh, F &&f) {
 
 // row rhs of a contact normal (btSequentialImpulseConstraintSolver setup:
 // speculative margin when separated, ERP/split-impulse when penetrating)
+// (1/dt = 500 is exact in fp32: products with it instead of IEEE divisions
+// by the rounded dt, and closer to the fp64 oracle's pen / dt)
+constexpr float PS_INV_DT = (float)(1.0 / PM_TIMESTEP);
 PS_D float normal_rhs(float dist, float rel, float dinv) {
-    const float dt = (float)PM_TIMESTEP;
     float pen = dist + (float)PM_LINEAR_SLOP;
     float velerr = -rel, poserr = 0.0f;
-    if (pen > 0.0f) velerr -= pen / dt;
-    else poserr = -pen * (float)PM_ERP / dt;
+    if (pen > 0.0f) velerr -= pen * PS_INV_DT;
+    else poserr = -pen * (float)PM_ERP * PS_INV_DT;
     bool combined = pen > (float)PM_SPLIT_PENETRATION_THRESHOLD;
     return (combined ? poserr + velerr : velerr) * dinv;
 }
 
-PS_D float safe_inv(float den) { return den > 2.2204460492503131e-16f ? 1.0f / den : 0.0f; }
+// 1/den of a row (v_rcp_f32, 1 ulp: an IEEE division is ~10 VALU
+// instructions, and the substep takes ~35 of these)
+PS_D float safe_inv(float den) { return den > 2.2204460492503131e-16f ? __builtin_amdgcn_rcpf(den) : 0.0f; }
 
 // Stack: 1/den of a cube's ground row j (normal +z, then (0,-1,0), (1,0,0))
 // from its contact offset r: den = |r x dir|^2 iI + 1/m (isotropic inertia);
@@ -1856,7 +1868,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
 #pragma unroll
     for (int d = 0; d < 9; d++) {
         float den = Mi[sidx(d, d)];
-        dinvj[d] = den > 2.2204460492503131e-16f ? 1.0f / den : 0.0f;
+        dinvj[d] = safe_inv(den);
         split_dq[d] = 0.0f;
         lim_rhs[d] = 0.0f;
         lim_lam[d] = 0.0f;
@@ -1868,7 +1880,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             bool on = pen <= 0.0f;
             float velerr = -sgn * v1[d];
             bool combined = pen > (float)PM_SPLIT_PENETRATION_THRESHOLD;
-            float poserr = -pen * (float)PM_ERP / dt;
+            float poserr = -pen * (float)PM_ERP * PS_INV_DT;
             if (on) {
                 lim_on |= 1u << d;
                 lim_up |= side ? 1u << d : 0u;
@@ -1878,7 +1890,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         }
         float kp = STD_MOTORS ? (float)PM_MOTOR_KP : mt.kp[d], kd = STD_MOTORS ? (float)PM_MOTOR_KD : mt.kd[d];
         float vel = STD_MOTORS ? 0.0f : mt.vel[d];
-        float target = kp * (mt.target[d] - q[d]) / dt + v1[d] + kd * (vel - v1[d]);
+        float target = kp * (mt.target[d] - q[d]) * PS_INV_DT + v1[d] + kd * (vel - v1[d]);
         mot_rhs[d] = (target - v1[d]) * dinvj[d];
         mot_lam[d] = 0.0f;
     }
