@@ -1874,8 +1874,16 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         lim_lam[d] = 0.0f;
 #pragma unroll
         for (int side = 0; side < 2; side++) {
-            float lo = (float)dof_def(d).lo, hi = (float)dof_def(d).hi;
-            float pen = side ? hi - q[d] : q[d] - lo;
+            // the limit as fp32 head + tail (lo = lo_h + lo_t): q - lo_h is
+            // exact near the limit, so the row switches where the fp64 limit
+            // puts it (a joint pressed onto -3.0718 by its motor sits exactly
+            // at fp32(-3.0718) = -3.0717999935, 6.5e-9 inside the double
+            // limit: on with the fp32 constant, off in Bullet and the oracle)
+            // (folded to constants: the loop is unrolled)
+            const double LO = dof_def(d).lo, HI = dof_def(d).hi;
+            const float lo_h = (float)LO, lo_t = (float)(LO - (double)lo_h);
+            const float hi_h = (float)HI, hi_t = (float)(HI - (double)hi_h);
+            float pen = side ? (hi_h - q[d]) + hi_t : (q[d] - lo_h) - lo_t;
             float sgn = side ? -1.0f : 1.0f;
             bool on = pen <= 0.0f;
             float velerr = -sgn * v1[d];

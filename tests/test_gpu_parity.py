@@ -208,6 +208,24 @@ def _object_rows(task):
 OBJ_ATOL = {"push": 5e-4, "slide": 5e-4}
 
 
+def _sim_step_sensitivity(cfg, snap, i, ref):
+    """Largest move of the oracle's joint positions and velocities after one
+    engine step (20 substeps) from env i of `snap` under one fp32 ulp of
+    state noise per substep (four seeds) and with the state rounded to fp32
+    every substep (test_gpu_parity._sensitivity for the engine step)."""
+    sq = sqd = 0.0
+    try:
+        for ulps, seed in [(1.0, 1), (1.0, 2), (1.0, 3), (1.0, 4), (-1.0, 0)]:
+            O.set_state_noise(ulps, seed)
+            e = oracle_env_from(cfg, snap, i)
+            O.sim_step(cfg, e)
+            sq = max(sq, float(np.abs(np.array(e.q) - np.array(ref.q)).max()))
+            sqd = max(sqd, float(np.abs(np.array(e.qd) - np.array(ref.qd)).max()))
+    finally:
+        O.set_state_noise(0.0)
+    return sq, sqd
+
+
 @pytest.mark.parametrize("task", ALL_TASKS)
 def test_sim_step_parity_same_motors(ps, task):
     """Engine step (20 substeps) from identical joints, motors and object."""
@@ -217,7 +235,7 @@ def test_sim_step_parity_same_motors(ps, task):
     env.reset(seed=21)
     cfg = oracle_config_for(env.sim.cfg)
     rng = np.random.default_rng(5)
-    err_q, err_qd = [], []
+    err_q, err_qd, conditioned = [], [], []
     for s in range(8):
         env.step(torch.from_numpy(rng.uniform(-1, 1, size=(B, env.action_dim)).astype(np.float32)).cuda())
         snap = snapshot(env.sim)  # motors hold the targets of this step's set_action
@@ -226,19 +244,30 @@ def test_sim_step_parity_same_motors(ps, task):
         for i in range(0, B, 4):
             e = oracle_env_from(cfg, snap, i)
             O.sim_step(cfg, e)
-            err_q.append(np.abs(after["f"][0:9, i] - np.array(e.q)).max())
-            err_qd.append(np.abs(after["f"][9:18, i] - np.array(e.qd)).max())
+            eq = np.abs(after["f"][0:9, i] - np.array(e.q)).max()
+            eqd = np.abs(after["f"][9:18, i] - np.array(e.qd)).max()
+            err_q.append(eq)
+            err_qd.append(eqd)
+            cond = False
+            if eq >= SIM_TIGHT["q"] or eqd >= SIM_TIGHT["qd"]:
+                # within the tight bounds once NOISE_K x the oracle's own
+                # spread at the state's fp32 resolution is allowed for (_judge)
+                sq, sqd = _sim_step_sensitivity(cfg, snap, i, e)
+                cond = eq < SIM_TIGHT["q"] + NOISE_K * sq and eqd < SIM_TIGHT["qd"] + NOISE_K * sqd
+            conditioned.append(cond)
             for b, row in enumerate(_object_rows(task)):
                 assert np.allclose(after["f"][row:row + 3, i], np.array(e.obj[b].pos),
                                    atol=OBJ_ATOL.get(task, 5e-3)), (s, i, b)
-    err_q, err_qd = np.array(err_q), np.array(err_qd)
+    err_q, err_qd, conditioned = np.array(err_q), np.array(err_qd), np.array(conditioned)
     tight = (err_q < SIM_TIGHT["q"]) & (err_qd < SIM_TIGHT["qd"])
-    print(task, f"max q {err_q.max():.1e} qd {err_qd.max():.1e}; tight {tight.mean() * 100:.1f} % of {tight.size}")
+    print(task, f"max q {err_q.max():.1e} qd {err_qd.max():.1e}; tight {tight.mean() * 100:.1f} % of {tight.size}, "
+                f"within the oracle's conditioning {conditioned.sum()}")
     if task in FREE_GRIPPER:
         assert tight.mean() >= 0.95
         assert err_q.max() < SIM_LOOSE["q"] and err_qd.max() < SIM_LOOSE["qd"]
     else:
-        assert tight.all(), (err_q.max(), err_qd.max())
+        assert (tight | conditioned).all(), (err_q.max(), err_qd.max())
+        assert conditioned.mean() <= 0.02
 
 
 # Per-component tolerances of the fused env step (fp32 GPU vs fp64 oracle from
@@ -399,8 +428,10 @@ def _judge(cfg, snap, i, action, o, og, groups, task):
     """Classifies one teacher-forced sample (GPU observation og vs oracle o):
     'tight' within the tight bounds; 'conditioned' within them once NOISE_K x
     the oracle's sensitivity is added; 'bif' at a branch the oracle itself
-    cannot resolve at fp32 resolution (_ill_conditioned: held to the loose
-    bounds); 'beyond' otherwise.  Returns (class, per-group errors)."""
+    cannot resolve at fp32 resolution (its answer leaves the tight bounds
+    under the state noise of _sensitivity, or under _ill_conditioned's probes:
+    held to the loose bounds); 'beyond' otherwise.  Returns (class, per-group
+    errors)."""
     tol = TOL[task]
     errs = {k: _obs_err(og, o, k, idx, task) for k, idx in groups.items()}
     bad = [k for k in groups if not _within(errs[k], o, groups, k, tol)]
@@ -409,7 +440,11 @@ def _judge(cfg, snap, i, action, o, og, groups, task):
     sens = _sensitivity(cfg, snap, i, action, o, groups, task)
     if all(_within(errs[k] - NOISE_K * sens[k], o, groups, k, tol) for k in bad):
         return "conditioned", errs
-    if _ill_conditioned(cfg, snap, i, action, o, groups, tol, task):
+    # the oracle's own answer leaves the tight bounds under fp32-resolution
+    # state noise (a limit row or contact that flickers on some substeps and
+    # not on others), or under one of the probes
+    if any(not _within(sens[k], o, groups, k, tol) for k in groups) or \
+            _ill_conditioned(cfg, snap, i, action, o, groups, tol, task):
         return "bif", errs
     return "beyond", errs
 
