@@ -30,16 +30,41 @@ struct Kin {
 template <int I>
 PS_D Frame child_frame(const Frame &P, float q) {
     constexpr LinkDef d = link_def(I);
-    constexpr M3d Ro = origin_rot(I);
     Frame F;
     M3 Rj;
-#pragma unroll
-    for (int r = 0; r < 3; r++)
-#pragma unroll
-        for (int c = 0; c < 3; c++)
-            Rj.m[r * 3 + c] = P.R.m[r * 3 + 0] * (float)Ro.m[0 * 3 + c] + P.R.m[r * 3 + 1] * (float)Ro.m[1 * 3 + c] +
-                              P.R.m[r * 3 + 2] * (float)Ro.m[2 * 3 + c];
-    V3 oj = P.o + mul(P.R, mk((float)d.o[0], (float)d.o[1], (float)d.o[2]));
+    // P.R times the constant joint-origin rotation and offset with the zero
+    // terms dropped at compile time (IEEE x * 0 is not folded, and the
+    // origins are axis permutations or identities: 18 of the 27 products
+    // were zeros, in every one of the ~60 frames an env-step builds)
+    static_for<0, 3>([&](auto RR) {
+        constexpr int r = decltype(RR)::value;
+        static_for<0, 3>([&](auto CC) {
+            constexpr int c = decltype(CC)::value;
+            float acc = 0.0f;
+            bool any = false;
+            static_for<0, 3>([&](auto KK) {
+                constexpr int k = decltype(KK)::value;
+                constexpr double w = origin_rot(I).m[k * 3 + c];
+                if constexpr (w != 0.0) {
+                    const float t = w == 1.0 ? P.R.m[r * 3 + k] : (w == -1.0 ? -P.R.m[r * 3 + k] : P.R.m[r * 3 + k] * (float)w);
+                    acc = any ? acc + t : t;
+                    any = true;
+                }
+            });
+            Rj.m[r * 3 + c] = acc;
+        });
+    });
+    V3 off = mk(0.0f, 0.0f, 0.0f);
+    bool anyo = false;
+    static_for<0, 3>([&](auto KK) {
+        constexpr int k = decltype(KK)::value;
+        if constexpr (d.o[k] != 0.0) {
+            const V3 t = col(P.R, k) * (float)d.o[k];
+            off = anyo ? off + t : t;
+            anyo = true;
+        }
+    });
+    V3 oj = P.o + off;
     if constexpr (d.type == PM_JOINT_REVOLUTE) {
         // libm sincosf (its range-reduction branch doubles as a scheduling
         // fence; __sinf/__cosf measured 12% slower on Push through spills)
@@ -62,6 +87,23 @@ PS_D Frame child_frame(const Frame &P, float q) {
         F.o = oj;
     }
     return F;
+}
+
+// R times link I's constant COM offset, zero terms dropped at compile time
+template <int I>
+PS_D V3 com_offset(const M3 &R) {
+    constexpr LinkDef d = link_def(I);
+    V3 off = mk(0.0f, 0.0f, 0.0f);
+    bool any = false;
+    static_for<0, 3>([&](auto KK) {
+        constexpr int k = decltype(KK)::value;
+        if constexpr (d.com[k] != 0.0) {
+            const V3 t = col(R, k) * (float)d.com[k];
+            off = any ? off + t : t;
+            any = true;
+        }
+    });
+    return off;
 }
 
 // all link frames, base-relative (robot base at the origin, identity rotation)
@@ -95,7 +137,7 @@ PS_D V3 dof_axis(const Kin &k) {
 template <int I>
 PS_D V3 com_pos(const Kin &k) {
     constexpr LinkDef d = link_def(I);
-    return k.f[I].o + mul(k.f[I].R, mk((float)d.com[0], (float)d.com[1], (float)d.com[2]));
+    return k.f[I].o + com_offset<I>(k.f[I].R);
 }
 
 // ------------------------------------------------------------------ dynamics
@@ -171,7 +213,7 @@ template <int I>
 PS_D void link_wrench_f(const Frame &f, V3 w, V3 dw, V3 vo, V3 ao, V3 &F, V3 &N) {
     constexpr LinkDef d = link_def(I);
     constexpr float m = (float)d.mass;
-    V3 c = f.o + mul(f.R, mk((float)d.com[0], (float)d.com[1], (float)d.com[2]));
+    V3 c = f.o + com_offset<I>(f.R);
     V3 rc = c - f.o;
     V3 vc = vo + cross(w, rc);
     V3 ac = ao + cross(dw, rc) + cross(w, cross(w, rc));
