@@ -357,7 +357,8 @@ PS_D void inverse_kinematics(const float q_start[9], V3 target, Q4 orn, float q_
         diff = norm(dS);
         Q4 qe = mat_to_quat(k.f[LINK].R);
         float n2 = qe.x * qe.x + qe.y * qe.y + qe.z * qe.z + qe.w * qe.w;
-        Q4 qinv = Q4{-qe.x / n2, -qe.y / n2, -qe.z / n2, qe.w / n2};
+        const float in2 = 1.0f / n2;
+        Q4 qinv = Q4{-qe.x * in2, -qe.y * in2, -qe.z * in2, qe.w * in2};
         Q4 dq = qmul(ot, qinv);
         // btQuaternion::getAngle()/getAxis() evaluate 2 acos(w) and
         // v / sqrt(1 - w^2); for a unit quaternion these equal 2 atan2(|v|, w)
