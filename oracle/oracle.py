@@ -276,6 +276,12 @@ def set_finger_noise(amplitude: float, seed: int = 0):
     lib().po_set_finger_noise(float(amplitude), int(seed))
 
 
+def set_fp32_solver(on: bool):
+    """Test hook: round the PGS's accumulated impulses and velocity change to
+    fp32 after every row update (panda_oracle.c po_set_fp32_solver)."""
+    lib().po_set_fp32_solver(int(bool(on)))
+
+
 def set_link_aabb(link, lx, ly, lz):
     lib().po_set_link_aabb(link, lx, ly, lz)
 

@@ -1325,6 +1325,20 @@ static void contact_row_jac(const okin *k, const po_env *env, const ocontact *c,
     }
 }
 
+/* Test hook (never part of the restated algorithm): with fp32_solver set,
+ * the solver's running state -- each row's accumulated impulse and the
+ * velocity change -- is rounded to fp32 after every row update, as the GPU's
+ * fp32 solve keeps it.  The parity tests use it to see how far the solve
+ * itself moves at fp32 resolution (a non-converged 50-iteration PGS on an
+ * ill-conditioned row set amplifies it; tests/test_gpu_parity.py _sensitivity). */
+static int fp32_solver = 0;
+void po_set_fp32_solver(int on) { fp32_solver = on; }
+static double r32(double x) { return fp32_solver ? (double)(float)x : x; }
+static void r32v(double *v, int n) {
+    if (fp32_solver)
+        for (int k = 0; k < n; k++) v[k] = (double)(float)v[k];
+}
+
 static double row_dot(const double *a, const double *b) {
     double s = 0.0;
     for (int d = 0; d < ND; d++) s += a[d] * b[d];
@@ -1339,7 +1353,9 @@ static double solve_row(orow *r, double dv[ND]) {
     if (sum < r->lo) { dl = r->lo - r->lam; r->lam = r->lo; }
     else if (sum > r->hi) { dl = r->hi - r->lam; r->lam = r->hi; }
     else r->lam = sum;
+    r->lam = r32(r->lam);
     for (int d = 0; d < ND; d++) dv[d] += r->MJ[d] * dl;
+    r32v(dv, ND);
     return dl / r->dinv;
 }
 
@@ -1358,9 +1374,10 @@ static double solve_cone(orow *a, orow *b, double lam_n, double dv[ND]) {
     }
     dla = sa - a->lam;
     dlb = sb - b->lam;
-    a->lam = sa;
-    b->lam = sb;
+    a->lam = r32(sa);
+    b->lam = r32(sb);
     for (int d = 0; d < ND; d++) dv[d] += a->MJ[d] * dla + b->MJ[d] * dlb;
+    r32v(dv, ND);
     double ra = a->dinv != 0.0 ? dla / a->dinv : 0.0, rb = b->dinv != 0.0 ? dlb / b->dinv : 0.0;
     return fabs(ra) > fabs(rb) ? ra : rb;
 }

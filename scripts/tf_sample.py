@@ -36,7 +36,8 @@ def replay(path):
     fa = d["gpu_f_after"]
     dq = np.abs(fa[0:9] - np.array(e.q[:9]))
     dqd = np.abs(fa[9:18] - np.array(e.qd[:9]))
-    print(f"   q  err {np.array2string(dq, precision=1)}\n   qd err {np.array2string(dqd, precision=1)}")
+    fmt = {"float_kind": lambda x: f"{x:.1e}"}
+    print(f"   q  err {np.array2string(dq, formatter=fmt)}\n   qd err {np.array2string(dqd, formatter=fmt)}")
     gc, oc = gpu_cache(fa[:, None], 0), oracle_cache(e)
     for k in gc:
         print(f"   {k:8s} gpu {[(int(i), round(float(l), 5)) for i, l in gc[k]] if k != 'pair' else len(gc[k])}")
