@@ -282,6 +282,11 @@ def set_fp32_solver(on: bool):
     lib().po_set_fp32_solver(int(bool(on)))
 
 
+def set_fp32_dynamics(on: bool):
+    """Test hook: M^-1 in fp32 arithmetic (panda_oracle.c po_set_fp32_dynamics)."""
+    lib().po_set_fp32_dynamics(int(bool(on)))
+
+
 def set_link_aabb(link, lx, ly, lz):
     lib().po_set_link_aabb(link, lx, ly, lz)
 

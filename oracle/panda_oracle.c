@@ -421,6 +421,44 @@ static void spd_inverse(const double A[81], double Ai[81]) {
     }
 }
 
+/* Test hook (never part of the restated algorithm): with fp32_dynamics set,
+ * M^-1 is computed in fp32 from M rounded to fp32 (the GPU's Cholesky: one
+ * reciprocal per pivot), so the parity tests can see how far the arm's
+ * ill-conditioned mass matrix amplifies fp32 arithmetic. */
+static int fp32_dynamics = 0;
+void po_set_fp32_dynamics(int on) { fp32_dynamics = on; }
+static void spd_inverse_f32(const double A[81], double Ai[81]) {
+    float L[81], inv[9];
+    memset(L, 0, sizeof L);
+    for (int i = 0; i < 9; i++)
+        for (int j = 0; j <= i; j++) {
+            float t = (float)A[i * 9 + j];
+            for (int k = 0; k < j; k++) t -= L[i * 9 + k] * L[j * 9 + k];
+            if (i == j) {
+                L[i * 9 + i] = sqrtf(t);
+                inv[i] = 1.0f / L[i * 9 + i];
+            } else {
+                L[i * 9 + j] = t * inv[j];
+            }
+        }
+    float Li[81];
+    memset(Li, 0, sizeof Li);
+    for (int i = 0; i < 9; i++) {
+        Li[i * 9 + i] = inv[i];
+        for (int j = 0; j < i; j++) {
+            float t = 0.0f;
+            for (int q = j; q < i; q++) t += L[i * 9 + q] * Li[q * 9 + j];
+            Li[i * 9 + j] = -t * inv[i];
+        }
+    }
+    for (int i = 0; i < 9; i++)
+        for (int j = 0; j <= i; j++) {
+            float t = 0.0f;
+            for (int q = i; q < 9; q++) t += Li[q * 9 + i] * Li[q * 9 + j];
+            Ai[i * 9 + j] = Ai[j * 9 + i] = (double)t;
+        }
+}
+
 /* Gaussian elimination with partial pivoting (MatrixRmn::Solve). */
 static void ge_solve(int n, double *A, double *b, double *x) {
     for (int c = 0; c < n; c++) {
@@ -1549,7 +1587,8 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
         double M[81], hb[9];
         mass_matrix(&k, M);
         bias_forces(&k, env->qd, hb);
-        spd_inverse(M, Minv);
+        if (fp32_dynamics) spd_inverse_f32(M, Minv);
+        else spd_inverse(M, Minv);
         for (int a = 0; a < 9; a++) {
             double s = 0.0;
             for (int b = 0; b < 9; b++) s -= Minv[a * 9 + b] * hb[b];
