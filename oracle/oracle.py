@@ -118,6 +118,7 @@ def lib():
         L.po_link_inertia.argtypes = [I, P(D)]
         L.po_set_link_aabb.argtypes = [I, D, D, D]
         L.po_set_finger_noise.argtypes = [D, C.c_uint64]
+        L.po_set_finger_bias.argtypes = [D]
         L.po_set_state_noise.argtypes = [D, C.c_uint64]
         L.po_set_pgs_log.argtypes = [C.c_void_p, C.c_int64]
         L.po_set_pgs_log.restype = C.c_int64
@@ -274,6 +275,12 @@ def bias_forces(cfg, q, qd):
 def set_finger_noise(amplitude: float, seed: int = 0):
     """Test hook: per-substep finger-position noise (panda_oracle.c)."""
     lib().po_set_finger_noise(float(amplitude), int(seed))
+
+
+def set_finger_bias(b: float):
+    """Test hook: a constant per-substep offset b of both finger positions
+    (panda_oracle.c po_set_finger_bias)."""
+    lib().po_set_finger_bias(float(b))
 
 
 def set_fp32_solver(on: bool):

@@ -1503,6 +1503,11 @@ void po_set_finger_noise(double amplitude, uint64_t seed) {
     finger_noise_amp = amplitude;
     finger_noise_state = seed;
 }
+/* ... and a constant per-substep offset of the finger positions (both the
+ * same sign): the deterministic counterpart of the noise, for a finger limit
+ * row that flips on one particular substep */
+static double finger_bias = 0.0;
+void po_set_finger_bias(double b) { finger_bias = b; }
 static double finger_noise(void) {
     uint64_t z = (finger_noise_state += 0x9E3779B97F4A7C15ULL);
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -1787,8 +1792,8 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
             env->qd[d] = v1[d] + dv[d];
             env->q[d] += dt * env->qd[d] + split_dq[d];
         }
-        if (finger_noise_amp != 0.0)
-            for (int d = 7; d < 9; d++) env->q[d] += finger_noise();
+        if (finger_noise_amp != 0.0 || finger_bias != 0.0)
+            for (int d = 7; d < 9; d++) env->q[d] += finger_noise() + finger_bias;
     }
     if (state_noise_ulps != 0.0 && cfg->has_robot) {
         ulp_noise(env->q, 9);

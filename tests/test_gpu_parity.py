@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import oracle_config_for, oracle_env_from, snapshot
+from helpers import OBJECT_ROWS, oracle_config_for, oracle_env_from, snapshot
 
 import oracle as O
 
@@ -344,18 +344,33 @@ FP32_PROBES = _fp32_probes()
 STEP_DT = 20 / 500  # one env step: 20 substeps of 1/500 s (core.py n_substeps, timestep)
 
 
-def _within(err, o, groups, k, tol):
+def _within(err, o, groups, k, tol, before=None):
     """err <= tol[k], relative for the object velocities: an impact that spins
-    a cube up to ~30 rad/s within one step is resolved by the 50-iteration PGS
-    to ~1e-4 relative, so their bound is atol + 1e-3 |ref|; an object's
-    rotation accrues that angular-velocity allowance over the step
-    (+ STEP_DT x 1e-3 |omega|)."""
+    a cube up to ~30 rad/s within one step -- or stops such a spin: `before`
+    holds the groups' magnitudes at the start of the step -- is resolved by
+    the 50-iteration PGS to ~1e-4 relative, so their bound is atol + 1e-3 x
+    the larger magnitude; an object's rotation accrues that angular-velocity
+    allowance over the step (+ STEP_DT x 1e-3 |omega|)."""
+    before = before or {}
     bound = tol[k]
     if k.startswith("obj") and k.endswith(("_vel", "_avel")):
-        bound += 1e-3 * np.abs(o[groups[k]]).max()
+        bound += 1e-3 * max(np.abs(o[groups[k]]).max(), before.get(k, 0.0))
     if k.startswith("obj") and k.endswith("_rot"):
-        bound += STEP_DT * 1e-3 * np.linalg.norm(o[groups[k[:-4] + "_avel"]])
+        ka = k[:-4] + "_avel"
+        bound += STEP_DT * 1e-3 * max(np.linalg.norm(o[groups[ka]]), before.get(ka, 0.0))
     return err <= bound
+
+
+def _before(snap, i, task):
+    """The objects' velocity magnitudes (largest component) at the start of
+    the step, keyed like _groups (for _within)."""
+    out = {}
+    f = snap["f"][:, i]
+    for b, r in enumerate(OBJECT_ROWS[:{"reach": 0, "stack": 2}.get(task, 1)]):
+        p = "obj_" if b == 0 else "obj2_"
+        out[p + "vel"] = float(np.abs(f[r + 7:r + 10]).max())
+        out[p + "avel"] = float(np.abs(f[r + 10:r + 13]).max())
+    return out
 
 
 def _euler_matrix(e):
@@ -383,38 +398,45 @@ def _ill_conditioned(cfg, snap, i, action, o_ref, groups, tol, task=""):
     to the tight bounds at fp32 resolution: one of FP32_PROBES (the state
     changed at fp32 resolution) or a per-substep finger-position noise of
     4e-9 m -- one fp32 ulp of the finger range, the resolution at which the
-    fp32 path places a finger pressed against its limit (oracle.set_finger_noise)
-    -- moves its observation beyond them."""
-    runs = [(p, None) for p in FP32_PROBES] + [(None, seed) for seed in range(4)]
+    fp32 path places a finger pressed against its limit (oracle.set_finger_noise),
+    or a constant 4e-9 m per-substep offset of the fingers either way
+    (oracle.set_finger_bias: a finger limit row that flips on one substep, e.g.
+    the substep a blocked finger strikes the table) -- moves its observation
+    beyond them."""
+    runs = ([(p, None, 0.0) for p in FP32_PROBES] + [(None, seed, 0.0) for seed in range(4)] +
+            [(None, None, b) for b in (4e-9, -4e-9)])
     try:
-        for probe, seed in runs:
+        for probe, seed, bias in runs:
             e = oracle_env_from(cfg, snap, i)
             if probe is not None:
                 probe(e)
             O.set_finger_noise(4e-9 if seed is not None else 0.0, 0 if seed is None else seed)
+            O.set_finger_bias(bias)
             o, *_ = O.step(cfg, e, action)
-            if any(not _within(_obs_err(o, o_ref, k, idx, task), o_ref, groups, k, tol) for k, idx in groups.items()):
+            if any(not _within(_obs_err(o, o_ref, k, idx, task), o_ref, groups, k, tol, _before(snap, i, task))
+                   for k, idx in groups.items()):
                 return True
     finally:
         O.set_finger_noise(0.0)
+        O.set_finger_bias(0.0)
     return False
 
 
 # Conditioning-scaled bound: a sample beyond the tight bounds is still within
-# them once NOISE_K x the oracle's own sensitivity to the fp32 resolution of
-# the state is allowed for -- the largest move of its observation over four
-# runs with one fp32 ulp of noise on every state component per substep and one
-# run whose state is rounded to fp32 after every substep (the GPU's state
-# storage; oracle.set_state_noise).  NOISE_K is the pre-event free runs' ratio
-# (tests/test_gpu_contacts.py PRE_EVENT_ULP_RATIO): the fp32 path rounds its
-# arithmetic as well as its state, measured at <= 2x the state's effect.
+# them once the oracle's own sensitivity to the fp32 resolution of the state is
+# allowed for -- the largest move of its observation over four runs with
+# NOISE_K fp32 ulps of noise on every state component per substep and one run
+# whose state is rounded to fp32 after every substep (the GPU's state storage;
+# oracle.set_state_noise).  NOISE_K = 2: the fp32 path rounds its arithmetic as
+# well as its state, and the free runs' yardstick uses the same two ulps
+# (tests/test_gpu_contacts.py ULP_NOISE, scripts/free_run_yardstick.py).
 NOISE_K = 2.0
 
 
 def _sensitivity(cfg, snap, i, action, o_ref, groups, task):
     sens = {k: 0.0 for k in groups}
     try:
-        for ulps, seed in [(1.0, 1), (1.0, 2), (1.0, 3), (1.0, 4), (-1.0, 0)]:
+        for ulps, seed in [(NOISE_K, 1), (NOISE_K, 2), (NOISE_K, 3), (NOISE_K, 4), (-1.0, 0)]:
             O.set_state_noise(ulps, seed)
             o, *_ = O.step(cfg, oracle_env_from(cfg, snap, i), action)
             for k, idx in groups.items():
@@ -426,24 +448,25 @@ def _sensitivity(cfg, snap, i, action, o_ref, groups, task):
 
 def _judge(cfg, snap, i, action, o, og, groups, task):
     """Classifies one teacher-forced sample (GPU observation og vs oracle o):
-    'tight' within the tight bounds; 'conditioned' within them once NOISE_K x
-    the oracle's sensitivity is added; 'bif' at a branch the oracle itself
+    'tight' within the tight bounds; 'conditioned' within them once the
+    oracle's sensitivity (_sensitivity) is added; 'bif' at a branch the oracle itself
     cannot resolve at fp32 resolution (its answer leaves the tight bounds
     under the state noise of _sensitivity, or under _ill_conditioned's probes:
     held to the loose bounds); 'beyond' otherwise.  Returns (class, per-group
     errors)."""
     tol = TOL[task]
+    bf = _before(snap, i, task)
     errs = {k: _obs_err(og, o, k, idx, task) for k, idx in groups.items()}
-    bad = [k for k in groups if not _within(errs[k], o, groups, k, tol)]
+    bad = [k for k in groups if not _within(errs[k], o, groups, k, tol, bf)]
     if not bad:
         return "tight", errs
     sens = _sensitivity(cfg, snap, i, action, o, groups, task)
-    if all(_within(errs[k] - NOISE_K * sens[k], o, groups, k, tol) for k in bad):
+    if all(_within(errs[k] - sens[k], o, groups, k, tol, bf) for k in bad):
         return "conditioned", errs
     # the oracle's own answer leaves the tight bounds under fp32-resolution
     # state noise (a limit row or contact that flickers on some substeps and
     # not on others), or under one of the probes
-    if any(not _within(sens[k], o, groups, k, tol) for k in groups) or \
+    if any(not _within(sens[k], o, groups, k, tol, bf) for k in groups) or \
             _ill_conditioned(cfg, snap, i, action, o, groups, tol, task):
         return "bif", errs
     return "beyond", errs
