@@ -264,11 +264,20 @@ PS_HD constexpr double neutral_q(int d) {
 // the group: each step adds a value and its partner's, and a + b == b + a
 // (row_ror:8 pairs lanes i, i^8; row_half_mirror pairs j, 7-j within each
 // half row; quad_perm [1,0,3,2] and [2,3,0,1] pair i, i^1 and i, i^2).
+// (bound_ctrl: a lane whose source is out of its row reads 0 -- none is, for
+// the controls used here -- so the destination needs no zeroing move first,
+// as update_dpp's `old` operand did: one VALU op less per DPP read)
 template <int CTRL>
 PS_D float dpp_f(float x) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
 }
+// The additions are kept out of FMA contraction: with one DoF per lane the
+// summand is a product, and contracting `J v + dpp(J v)` into fma(J, v, dpp)
+// rounds this lane's term differently from the partner's copy of it, so the
+// lanes of a group would end with different bits (and could leave the PGS loop
+// on different iterations).
 PS_D float group16_sum(float x) {
+#pragma clang fp contract(off)
     x += dpp_f<0x128>(x);  // row_ror:8
     x += dpp_f<0x141>(x);  // row_half_mirror
     x += dpp_f<0xB1>(x);   // quad_perm [1,0,3,2]
@@ -287,6 +296,7 @@ PS_D float group16_bcast(float x) {
 // the same over groups of 8 lanes: half_mirror pairs lane i with 7 - i, then
 // the quad swaps (every lane of the group ends with the same bits)
 PS_D float group8_sum(float x) {
+#pragma clang fp contract(off)
     x += dpp_f<0x141>(x);  // row_half_mirror
     x += dpp_f<0xB1>(x);   // quad_perm [1,0,3,2]
     x += dpp_f<0x4E>(x);   // quad_perm [2,3,0,1]
