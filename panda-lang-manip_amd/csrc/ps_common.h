@@ -303,15 +303,14 @@ PS_D float group8_sum(float x) {
     return x;
 }
 
-// lane K of this lane's 8-lane group, in every lane of the group: lane K % 4
-// of each quad (quad_perm), and the other quad's value through half_mirror
+// lane K of this lane's 8-lane group, in every lane of the group: row_newbcast
+// of lane K and of lane 8 + K of the 16-lane row (two independent DPP reads),
+// the group's half selected by lane bit 3
 template <int K>
 PS_D float group8_bcast(float x) {
     static_assert(K >= 0 && K < 8, "lane of the group");
-    constexpr int q = K & 3;
-    const float y = dpp_f<q | (q << 2) | (q << 4) | (q << 6)>(x);
-    const float z = dpp_f<0x141>(y);
-    return ((__lane_id() & 4u) == (unsigned)(K & 4)) ? y : z;
+    const float lo = dpp_f<0x150 + K>(x), hi = dpp_f<0x158 + K>(x);
+    return (__lane_id() & 8u) ? hi : lo;
 }
 
 // compile-time loop

@@ -1431,23 +1431,30 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
     float dvm[K];  // this lane's velocity changes (DoFs e + k G)
 #pragma unroll
     for (int k = 0; k < K; k++) dvm[k] = 0.0f;
-    auto prod = [&](const float J[K]) {
-        float p = J[0] * dvm[0];
+    // KL: the first slot a row's J can be non-zero in.  The object's DoFs
+    // (9-14) sit in slots k >= 9 / G, so an object-only row (ground contacts)
+    // skips the slots below at compile time (IEEE 0 * x is not folded)
+    constexpr int KOBJ = 9 / G;
+    using KAll = std::integral_constant<int, 0>;
+    using KObj = std::integral_constant<int, KOBJ>;
+    auto prod = [&](auto KL, const float J[K]) {
+        constexpr int k0 = decltype(KL)::value;
+        float p = J[k0] * dvm[k0];
 #pragma unroll
-        for (int k = 1; k < K; k++) p = fmaf(J[k], dvm[k], p);
+        for (int k = k0 + 1; k < K; k++) p = fmaf(J[k], dvm[k], p);
         return p;
     };
-    auto apply = [&](const float M[K], float dl) {
+    auto apply = [&](auto KL, const float M[K], float dl) {
 #pragma unroll
-        for (int k = 0; k < K; k++) dvm[k] = fmaf(M[k], dl, dvm[k]);
+        for (int k = decltype(KL)::value; k < K; k++) dvm[k] = fmaf(M[k], dl, dvm[k]);
     };
     // warm start (see the one-lane solver)
 #pragma unroll
     for (int c = 0; c < NG; c++)
-        if (NOBJ > 0 && (gate_gnd & (1u << c))) apply(gM[c][0], gc[c].lam[0]);
+        if (NOBJ > 0 && (gate_gnd & (1u << c))) apply(KObj{}, gM[c][0], gc[c].lam[0]);
 #pragma unroll
     for (int c = 0; c < NR; c++)
-        if (gate_robot & (1u << c)) apply(rM[c][0], rc[c].lam[0]);
+        if (gate_robot & (1u << c)) apply(KAll{}, rM[c][0], rc[c].lam[0]);
 
     float res = 0.0f;
     // a joint row's J is e_d: its product is the velocity change of DoF d,
@@ -1480,19 +1487,19 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
     // rows d = 8..0 and 0..8 with compile-time d
     auto down = [&](auto row) { static_for<0, 9>([&](auto I) { row(std::integral_constant<int, 8 - decltype(I)::value>{}); }); };
     auto up = [&](auto row) { static_for<0, 9>([&](auto I) { row(I); }); };
-    auto normal = [&](const float Jm[K], const float Mm[K], float rhs, float dinv, float &lam) {
-        float s = group_sum<G>(prod(Jm));
+    auto normal = [&](auto KL, const float Jm[K], const float Mm[K], float rhs, float dinv, float &lam) {
+        float s = group_sum<G>(prod(KL, Jm));
         float dl = rhs - dinv * s;
         float nl = fminf(fmaxf(lam + dl, 0.0f), (float)PM_CONTACT_UPPER);
         dl = nl - lam;
         lam = nl;
         PS_REC(dl);
-        apply(Mm, dl);
+        apply(KL, Mm, dl);
         res = fmaxf(res, row_viol(dl, dinv));
     };
-    auto cone = [&](const float J[3][K], const float M[3][K], const float rhs[3], const float dinv[3], float lam[3],
-                    float mu) {
-        float sa = group_sum<G>(prod(J[1])), sb = group_sum<G>(prod(J[2]));
+    auto cone = [&](auto KL, const float J[3][K], const float M[3][K], const float rhs[3], const float dinv[3],
+                    float lam[3], float mu) {
+        float sa = group_sum<G>(prod(KL, J[1])), sb = group_sum<G>(prod(KL, J[2]));
         float dla = rhs[1] - dinv[1] * sa, dlb = rhs[2] - dinv[2] * sb;
         float a = lam[1] + dla, b = lam[2] + dlb;
         float lim = mu * fmaxf(lam[0], 0.0f);
@@ -1506,7 +1513,7 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         PS_REC(dla);
         PS_REC(dlb);
 #pragma unroll
-        for (int k = 0; k < K; k++) dvm[k] = fmaf(M[2][k], dlb, fmaf(M[1][k], dla, dvm[k]));
+        for (int k = decltype(KL)::value; k < K; k++) dvm[k] = fmaf(M[2][k], dlb, fmaf(M[1][k], dla, dvm[k]));
         res = fmaxf(res, fmaxf(row_viol(dla, dinv[1]), row_viol(dlb, dinv[2])));
     };
     // the object's ground normals touch only object DoFs: they commute with
@@ -1516,19 +1523,19 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
     auto ground_normals = [&]() {
         if constexpr (NOBJ > 0) {
 #pragma unroll
-            for (int c = 0; c < NG; c++) normal(gJ[c][0], gM[c][0], gc[c].rhs[0], gc[c].dinv[0], gc[c].lam[0]);
+            for (int c = 0; c < NG; c++) normal(KObj{}, gJ[c][0], gM[c][0], gc[c].rhs[0], gc[c].dinv[0], gc[c].lam[0]);
         }
     };
     auto contacts = [&]() {
 #pragma unroll
         for (int c = 0; c < NR; c++)
-            if (gate_robot & (1u << c)) normal(rJ[c][0], rM[c][0], rc[c].rhs[0], rc[c].dinv[0], rc[c].lam[0]);
+            if (gate_robot & (1u << c)) normal(KAll{}, rJ[c][0], rM[c][0], rc[c].rhs[0], rc[c].dinv[0], rc[c].lam[0]);
 #pragma unroll
         for (int c = 0; c < NG; c++)
-            if (NOBJ > 0 && (gate_gnd & (1u << c))) cone(gJ[c], gM[c], gc[c].rhs, gc[c].dinv, gc[c].lam, gmu);
+            if (NOBJ > 0 && (gate_gnd & (1u << c))) cone(KObj{}, gJ[c], gM[c], gc[c].rhs, gc[c].dinv, gc[c].lam, gmu);
 #pragma unroll
         for (int c = 0; c < NR; c++)
-            if (gate_robot & (1u << c)) cone(rJ[c], rM[c], rc[c].rhs, rc[c].dinv, rc[c].lam, rc[c].mu);
+            if (gate_robot & (1u << c)) cone(KAll{}, rJ[c], rM[c], rc[c].rhs, rc[c].dinv, rc[c].lam, rc[c].mu);
     };
     for (int it = 0; it < PM_SOLVER_ITERATIONS; it += 2) {
 #ifdef PS_PROFILE_PHASES
