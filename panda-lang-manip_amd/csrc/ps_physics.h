@@ -2256,12 +2256,12 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         for (int k = 0; k < n; k++) m |= __builtin_amdgcn_ballot_w64(pred(k)) ? 1u << k : 0u;
         return (unsigned)__builtin_amdgcn_readfirstlane((int)m);
     };
-    const unsigned gate_lim = wave_bits([&](int d) { return ((lim_on >> d) & 1u) != 0u; }, 9);
+    unsigned gate_lim = wave_bits([&](int d) { return ((lim_on >> d) & 1u) != 0u; }, 9);
     unsigned gate_ground[NB];
 #pragma unroll
     for (int b = 0; b < NB; b++) gate_ground[b] = wave_bits([&](int c) { return c < ng[b]; }, NG);
-    const unsigned gate_pair = wave_bits([&](int c) { return c < np; }, NP);
-    const unsigned gate_robot = wave_bits([&](int c) { return c < nr; }, NR);
+    unsigned gate_pair = wave_bits([&](int c) { return c < np; }, NP);
+    unsigned gate_robot = wave_bits([&](int c) { return c < nr; }, NR);
 
 #ifdef PS_PROFILE_PHASES
     int prof_it = 0;
@@ -2271,6 +2271,16 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
 #endif
     // the solver stops when every row's violation (row_viol, joint_viol) is <= 0
     static_assert(PM_SOLVER_ITERATIONS % 2 == 0, "iteration pairs");
+    // The gates are wave-uniform SGPR values.  Hoisted out of the PGS loop,
+    // whose exit is per lane, their bit tests become lane masks that are
+    // rebuilt against exec at every gated row (a v_cndmask + v_cmp pair
+    // each); redefining them at the top of each half-iteration (an empty asm
+    // with an "s" operand) keeps the tests scalar, inside the loop.
+#define PS_REGATE()                                                                        \
+    do {                                                                                   \
+        asm volatile("" : "+s"(gate_lim), "+s"(gate_pair), "+s"(gate_robot));              \
+        for (int b_ = 0; b_ < NB; b_++) asm volatile("" : "+s"(gate_ground[b_]));         \
+    } while (0)
     if constexpr (G == 1) {
     auto joint_row = [&](int d, float sgn, float rhs, float &lam, float lo, float hi) {
         float dl = rhs - dinvj[d] * (sgn * dv[d]);
@@ -2733,6 +2743,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         PS_COUNT_IT();
         L = lds.opaque();
         res = 0.0f;
+        PS_REGATE();
         // one object: M^-1 enters each iteration pair in VGPRs (an empty asm
         // with a "v" operand), else the allocator parks it in AGPRs and
         // every motor row reads its column back (v_accvgpr_read): the PGS
@@ -2756,6 +2767,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         PS_COUNT_IT();
         L = lds.opaque();
         res = 0.0f;
+        PS_REGATE();
         if (PS_GATE(gate_lim != 0u, 0)) {
 #pragma unroll
             for (int d = 0; d < 9; d++) limit_row(d);
