@@ -1537,11 +1537,15 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         for (int c = 0; c < NR; c++)
             if (gate_robot & (1u << c)) cone(KAll{}, rJ[c], rM[c], rc[c].rhs, rc[c].dinv, rc[c].lam, rc[c].mu);
     };
+    // (the gates stay scalar tests inside the loop, as in the one-lane
+    // solver's PS_REGATE)
+    auto regate = [&]() { asm volatile("" : "+s"(gate_lim), "+s"(gate_gnd), "+s"(gate_robot)); };
     for (int it = 0; it < PM_SOLVER_ITERATIONS; it += 2) {
 #ifdef PS_PROFILE_PHASES
         prof_it++;
 #endif
         res = 0.0f;
+        regate();
         down(motor_row);
         ground_normals();
         if (gate_lim != 0u) down(limit_row);
@@ -1551,6 +1555,7 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         prof_it++;
 #endif
         res = 0.0f;
+        regate();
         if (gate_lim != 0u) up(limit_row);
         up(motor_row);
         ground_normals();
