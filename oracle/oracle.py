@@ -122,6 +122,9 @@ def lib():
         L.po_set_state_noise.argtypes = [D, C.c_uint64]
         L.po_set_pgs_log.argtypes = [C.c_void_p, C.c_int64]
         L.po_set_pgs_log.restype = C.c_int64
+        L.po_set_model_mutation.argtypes = [I, D]
+        L.po_set_fp32_solver.argtypes = [I]
+        L.po_set_fp32_dynamics.argtypes = [I]
         _lib = L
     return _lib
 
@@ -296,6 +299,17 @@ def set_fp32_dynamics(on: bool):
 
 def set_link_aabb(link, lx, ly, lz):
     lib().po_set_link_aabb(link, lx, ly, lz)
+
+
+MUTATIONS = {"none": 0, "motor_kp_scale": 1, "link_damping": 2, "finger_box_grow": 3}
+
+
+def set_model_mutation(kind: str, value: float = 0.0):
+    """Test hook: a deliberate model error (panda_oracle.c po_set_model_mutation):
+    'motor_kp_scale' (kp x value), 'link_damping' (every body's k1 = k2 := value),
+    'finger_box_grow' (finger boxes' half extents + value m); 'none' restores
+    the model.  The object's mass and friction are Config fields."""
+    lib().po_set_model_mutation(MUTATIONS[kind], float(value))
 
 
 def set_state_noise(ulps: float, seed: int = 0):

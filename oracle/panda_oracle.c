@@ -105,6 +105,35 @@ void po_set_link_aabb(int link, double lx, double ly, double lz) {
     compute_inertia(&L[link]);
 }
 
+/* Test hook (never part of the restated algorithm): deliberate model errors,
+ * for showing that the parity classifier (tests/parity_judge.py) reports a
+ * wrong constant as a failure (tests/test_judge_power.py).  kind:
+ *   PO_MUT_NONE         restore every default;
+ *   PO_MUT_MOTOR_KP     scale POSITION_CONTROL's kp (PM_MOTOR_KP) by value;
+ *   PO_MUT_LINK_DAMPING btMultiBody damping (k1 = k2, linear and angular) of
+ *                       every body, the arm's links and the objects := value;
+ *   PO_MUT_FINGER_BOX   grow the finger boxes' half extents by value (m).
+ * The object's mass and lateral friction are po_config fields already. */
+static double mut_kp_scale = 1.0;
+static double mut_link_damping = PM_LINEAR_DAMPING;
+static double mut_finger_grow = 0.0;
+static void boxes_apply_mutation(void);
+void po_set_model_mutation(int kind, double value) {
+    model_init();
+    if (kind == PO_MUT_NONE) {
+        mut_kp_scale = 1.0;
+        mut_link_damping = PM_LINEAR_DAMPING;
+        mut_finger_grow = 0.0;
+    } else if (kind == PO_MUT_MOTOR_KP) {
+        mut_kp_scale = value;
+    } else if (kind == PO_MUT_LINK_DAMPING) {
+        mut_link_damping = value;
+    } else if (kind == PO_MUT_FINGER_BOX) {
+        mut_finger_grow = value;
+    }
+    boxes_apply_mutation();
+}
+
 /* --------------------------------------------------------------- algebra */
 static void v3_cross(const double a[3], const double b[3], double o[3]) {
     double x = a[1] * b[2] - a[2] * b[1], y = a[2] * b[0] - a[0] * b[2], z = a[0] * b[1] - a[1] * b[0];
@@ -357,8 +386,8 @@ static void bias_forces(const okin *k, const double qd[9], double h[9]) {
         m3_vec(Iw, w[i], Iww);
         m3_vec(Iw, dw[i], Idw);
         v3_cross(w[i], Iww, gyro);
-        double cl = PM_LINEAR_DAMPING + PM_LINEAR_DAMPING * v3_norm(vc);
-        double ca = PM_ANGULAR_DAMPING + PM_ANGULAR_DAMPING * v3_norm(w[i]);
+        double cl = mut_link_damping + mut_link_damping * v3_norm(vc);
+        double ca = mut_link_damping + mut_link_damping * v3_norm(w[i]); /* PM_ANGULAR_DAMPING = PM_LINEAR_DAMPING */
         double F[3], N[3];
         for (int d = 0; d < 3; d++) {
             F[d] = l->mass * ac[d] + l->mass * vc[d] * cl;
@@ -884,11 +913,25 @@ typedef struct {
     double c[3], h[3], mu;
 } obox_def;
 
-static const obox_def BOXES[PM_NUM_BOXES] = {
+static const obox_def BOXES_MODEL[PM_NUM_BOXES] = {
 #define OL_BOX(link_, cx, cy, cz, hx, hy, hz, mu_) {link_, {cx, cy, cz}, {hx, hy, hz}, mu_},
     PM_BOX_TABLE(OL_BOX)
 #undef OL_BOX
 };
+/* the boxes in use: the model's, or with the finger boxes (links 9, 10) grown
+ * by po_set_model_mutation's test hook */
+static obox_def BOXES[PM_NUM_BOXES] = {
+#define OL_BOX(link_, cx, cy, cz, hx, hy, hz, mu_) {link_, {cx, cy, cz}, {hx, hy, hz}, mu_},
+    PM_BOX_TABLE(OL_BOX)
+#undef OL_BOX
+};
+static void boxes_apply_mutation(void) {
+    for (int b = 0; b < PM_NUM_BOXES; b++) {
+        BOXES[b] = BOXES_MODEL[b];
+        if (BOXES[b].link == 9 || BOXES[b].link == 10)
+            for (int j = 0; j < 3; j++) BOXES[b].h[j] += mut_finger_grow;
+    }
+}
 
 /* world pose of box b: centre, rotation (columns = box axes) */
 static void robot_box(const okin *k, int b, double c[3], double R[9]) {
@@ -1609,8 +1652,8 @@ void po_substep(const po_config *cfg, po_env *env, po_stats *stats) {
         const po_body *b = &env->obj[i];
         object_setup(cfg, env, i, &ob[i]);
         int o = OBJ_DOF(i);
-        double cl = PM_LINEAR_DAMPING + PM_LINEAR_DAMPING * v3_norm(b->vel);
-        double ca = PM_ANGULAR_DAMPING + PM_ANGULAR_DAMPING * v3_norm(b->omg);
+        double cl = mut_link_damping + mut_link_damping * v3_norm(b->vel); /* PM_LINEAR_DAMPING */
+        double ca = mut_link_damping + mut_link_damping * v3_norm(b->omg); /* PM_ANGULAR_DAMPING */
         double gyro[3] = {0.0, 0.0, 0.0};
         if (!ob[i].iso) {
             double Iw[9], Iww[3], t[3];
@@ -1838,7 +1881,7 @@ void po_control_joints(po_env *env, int n, const int32_t *joints, const double *
         for (int j = 0; j < 9; j++) if (dof_link[j] == joints[i]) d = j;
         if (d < 0) continue;
         env->m_target[d] = targets[i];
-        env->m_kp[d] = PM_MOTOR_KP;
+        env->m_kp[d] = PM_MOTOR_KP * mut_kp_scale;
         env->m_kd[d] = PM_MOTOR_KD;
         env->m_vel[d] = 0.0;
         env->m_maximp[d] = forces[i] * PM_TIMESTEP;

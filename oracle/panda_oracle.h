@@ -154,6 +154,13 @@ void po_mass_matrix(const po_config *cfg, const double q[9], double M[81]);
 void po_bias_forces(const po_config *cfg, const double q[9], const double qd[9], double h[9]);
 void po_link_inertia(int link, double inertia[3]);
 void po_set_link_aabb(int link, double lx, double ly, double lz);
+/* test hook: deliberate model errors for the parity classifier's power test
+ * (tests/test_judge_power.py); PO_MUT_NONE restores the model, not thread-safe */
+#define PO_MUT_NONE 0
+#define PO_MUT_MOTOR_KP 1     /* kp := PM_MOTOR_KP x value */
+#define PO_MUT_LINK_DAMPING 2 /* btMultiBody damping k1 = k2 of every body := value */
+#define PO_MUT_FINGER_BOX 3   /* finger boxes' half extents += value (m) */
+void po_set_model_mutation(int kind, double value);
 /* test hook: per-substep finger-position noise of +-amplitude (0 = off), not thread-safe */
 void po_set_finger_noise(double amplitude, uint64_t seed);
 /* test hook: after every substep each state component x (q, qd, object pose

@@ -275,9 +275,13 @@ PS_D float dpp_f(float x) {
 // summand is a product, and contracting `J v + dpp(J v)` into fma(J, v, dpp)
 // rounds this lane's term differently from the partner's copy of it, so the
 // lanes of a group would end with different bits (and could leave the PGS loop
-// on different iterations).
+// on different iterations).  PS_EXPERIMENT_GROUP_SUM_CONTRACT (a diagnostic
+// build of scripts/build_variants.py, never the product) leaves contraction on,
+// to show what it does to the group kernels.
 PS_D float group16_sum(float x) {
+#ifndef PS_EXPERIMENT_GROUP_SUM_CONTRACT
 #pragma clang fp contract(off)
+#endif
     x += dpp_f<0x128>(x);  // row_ror:8
     x += dpp_f<0x141>(x);  // row_half_mirror
     x += dpp_f<0xB1>(x);   // quad_perm [1,0,3,2]
@@ -296,7 +300,9 @@ PS_D float group16_bcast(float x) {
 // the same over groups of 8 lanes: half_mirror pairs lane i with 7 - i, then
 // the quad swaps (every lane of the group ends with the same bits)
 PS_D float group8_sum(float x) {
+#ifndef PS_EXPERIMENT_GROUP_SUM_CONTRACT
 #pragma clang fp contract(off)
+#endif
     x += dpp_f<0x141>(x);  // row_half_mirror
     x += dpp_f<0xB1>(x);   // quad_perm [1,0,3,2]
     x += dpp_f<0x4E>(x);   // quad_perm [2,3,0,1]

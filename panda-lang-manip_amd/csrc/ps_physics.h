@@ -755,6 +755,7 @@ PS_D int pick_two(Visit &&visit, V3 org, V3 w, RCand &c0, RCand &c1) {
     RCand cmin = none, cmax = none;
     float s0 = 1e30f, vmin = 1e30f, vmax = -1e30f;
     c0 = none;
+    c1 = none;  // written for MAXN < 2 too (the caller copies it)
     visit([&](bool ok, const RCand &c) {
         const bool valid = ok && c.dist < margin;
         const float sv = dot(c.pA - org, w);
@@ -997,8 +998,11 @@ struct BoxCyl {
             const float dist = object_closest<SHAPE_CYL>(sc, lA, cl, nl);
             emit(true, lA, cl, nl, dist);
         }
-        // 2. side faces of the box vs the generator line facing them
-#pragma unroll 1
+        // 2. side faces of the box vs the generator line facing them (unrolled:
+        // with a loop counter the face's axis selects -- colsel(bR, ax),
+        // comp(xh, a1) -- became dynamic indices into the BoxCyl object, which
+        // then lived in 120 B of scratch in every Slide kernel, round 4)
+#pragma unroll
         for (int fc = 0; fc < 6; fc++) {
             const int ax = fc >> 1;
             const float sg = (fc & 1) ? -1.0f : 1.0f;

@@ -31,6 +31,9 @@ VARIANTS = {
     # the group objects at -O3
     "dump": ["-DPS_DEBUG_ROW_DUMP"],
     "groups_o3_dump": ["-DPS_DEBUG_ROW_DUMP"],
+    # the group sums with FMA contraction left on (the round-3 miscompute?
+    # DESIGN.md §12.6)
+    "group_contract": ["-DPS_EXPERIMENT_GROUP_SUM_CONTRACT"],
 }
 
 

@@ -44,7 +44,7 @@ def replay(path):
         print(f"   {'':8s} ora {[(int(i), round(float(l), 5)) for i, l in oc[k]] if k != 'pair' else len(oc[k])}")
     # the oracle's own conditioning: the same step with the state moved at fp32
     # resolution (test_gpu_parity.FP32_PROBES) and with per-substep state noise
-    from test_gpu_parity import FP32_PROBES
+    from parity_judge import FP32_PROBES
 
     moves = []
     for p in FP32_PROBES:

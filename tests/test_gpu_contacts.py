@@ -113,7 +113,7 @@ def test_contact_cache_parity(task):
     env.reset(seed=44)
     cfg = oracle_config_for(env.sim.cfg)
     policy = _push_policy(env, "object1" if task == "stack" else "object")
-    from test_gpu_parity import NOISE_K
+    from parity_judge import NOISE_K
 
     ids_equal = total = hits = n_cond = 0
     lam_err = []
@@ -141,7 +141,7 @@ def test_contact_cache_parity(task):
                 d = float(np.abs(np.subtract(pg, po)).max())
                 if d > 1e-4:
                     # the oracle's own spread of this point at the state's
-                    # fp32 resolution (test_gpu_parity._judge's perturbations)
+                    # fp32 resolution (parity_judge.judge's perturbations)
                     sens = _pair_point_sensitivity(cfg, snap, i, a[i], po, c)
                     print(f"  {task} step {s} env {i} pair point {c}: |GPU - oracle| {d:.1e} m, "
                           f"oracle spread {sens:.1e} m")
@@ -204,7 +204,7 @@ def test_reset_places_objects_at_rest(task):
 # substep (oracle.set_state_noise).  A second oracle run with this noise shows
 # how far two runs that differ only by fp32 rounding drift apart.  Two ulps:
 # the fp32 path rounds its arithmetic as well as its state, which the
-# per-step bounds allow for with the same factor (test_gpu_parity.NOISE_K);
+# per-step bounds allow for with the same factor (parity_judge.NOISE_K);
 # scripts/free_run_yardstick.py measures the ensembles on the CPU
 # (profiles/r04_free_run_yardstick.jsonl: with one ulp Push ee 87-92 %, with
 # two 83-84 %, with the state rounded to fp32 every substep 91 %).
@@ -390,13 +390,13 @@ def test_teacher_forced_200_steps(task, control):
     one oracle step from the same state.  Samples beyond the tight bounds are
     dumped (state before and after, action, GPU observation) to
     gpurun_out/tf200/ and listed; at most 0.1 % of env-steps may exceed them
-    (test_gpu_parity._judge: beyond the tight bounds even after the oracle's
+    (parity_judge.judge: beyond the tight bounds even after the oracle's
     own sensitivity to the state's fp32 resolution is allowed for, and not at
     a branch the oracle cannot resolve at that resolution), none the loose ones.
     The free-gripper runs (PickAndPlace, Stack, Flip) hold the gripper half
     open (action 0), as in the event-onset test, so the finger-limit
     bifurcations stay out."""
-    from test_gpu_parity import LOOSE, _groups, _judge
+    from parity_judge import LOOSE, groups_for as _groups, judge as _judge
 
     B, T = 64, 200
     env = make_env(task, control, B)
@@ -440,7 +440,9 @@ def test_teacher_forced_200_steps(task, control):
     print(task, control, counts, "worst (not ill-conditioned)", {k: f"{v:.2e}" for k, v in worst.items()},
           "beyond:", beyond[:20])
     assert counts["beyond"] <= 0.001 * B * T
-    assert counts["bif"] <= 0.02 * B * T
+    # measured at most 14 conditioned + 3 ill-conditioned of 12 800 (Push ee,
+    # profiles/r04p_pytest_gpu.log); ADVICE r04: cap them near that rate
+    assert counts["conditioned"] + counts["bif"] <= 0.0025 * B * T
 
 
 def test_event_onset_parity_at_bench_config():
@@ -494,7 +496,7 @@ def test_reach_at_config_size():
     """BASELINE config C2 (PandaReach, 4096 envs): finite bounded observations,
     exact TimeLimit/autoreset bookkeeping over 60 steps, then 32 sampled envs
     teacher-forced against the oracle."""
-    from test_gpu_parity import LOOSE, _groups, _judge
+    from parity_judge import LOOSE, groups_for as _groups, judge as _judge
 
     B = 4096
     for control in ("ee", "joints"):
@@ -521,7 +523,7 @@ def test_reach_at_config_size():
                 assert np.abs(og[i, 3:6] - o[3:6]).max() < 2e-3, (control, i)
                 continue
             # the tight bounds, or the oracle's own conditioning (a fingertip on
-            # the table, a joint at its limit: test_gpu_parity._judge)
+            # the table, a joint at its limit: parity_judge.judge)
             cls, errs = _judge(cfg, snap, i, a[i], o, og[i], _groups("reach", 6), "reach")
             counts[cls] += 1
             assert cls != "beyond", (control, i, errs)
@@ -540,7 +542,7 @@ def test_push_and_pick_and_place_at_config_size(task):
     ._judge): samples the oracle itself cannot resolve at fp32 resolution
     (finger- and joint-limit branches) are held to the loose bounds instead,
     at most 8 % of them."""
-    from test_gpu_parity import FREE_GRIPPER, LOOSE, _groups, _judge
+    from parity_judge import FREE_GRIPPER, LOOSE, done_flags_ok, groups_for as _groups, judge as _judge
 
     from pandasim.envs import PandaVecEnv
 
@@ -568,15 +570,27 @@ def test_push_and_pick_and_place_at_config_size(task):
     sample = np.linspace(0, B - 1, 64).astype(int)
     worst = {k: 0.0 for k in groups}
     counts = {"tight": 0, "conditioned": 0, "bif": 0, "beyond": 0}
+    flag_mismatch = terminated = 0
     for s in range(3):
         snap = snapshot(env.sim)
         a = torch.rand(B, env.action_dim, device="cuda", generator=g) * 2 - 1
         obs, r, te, tr, _ = env.step(a)
         og, a = obs["observation"].cpu().numpy(), a.cpu().numpy()
         te, tr = te.cpu().numpy(), tr.cpu().numpy()
+        agg = obs["achieved_goal"].cpu().numpy()
+        # every env's terminated flag is the reference's rule on its own
+        # achieved goal (core.py:285, push.py:89-91), bit for bit
+        from parity_judge import terminated_rule
+        goal = env.sim.goal[:3, :B].t().cpu().numpy()
+        rule = np.array([terminated_rule(task, agg[i], goal[i]) for i in range(B)])
+        assert np.array_equal(te.astype(bool), rule), (s, np.nonzero(te.astype(bool) != rule))
+        terminated += int(te.sum())
         for i in sample:
             o, ag, dg, rr, t_e, t_r = O.step(cfg, oracle_env_from(cfg, snap, i), a[i])
             assert t_r == bool(tr[i]), (s, i)
+            ok, mismatch = done_flags_ok(task, te[i], agg[i], t_e, ag, snap["goal"][:3, i])
+            assert ok, (s, i, bool(te[i]), t_e)
+            flag_mismatch += mismatch
             cls, errs = _judge(cfg, snap, i, a[i], o, og[i], groups, task)
             counts[cls] += 1
             assert cls != "beyond", (task, s, i, errs)
@@ -584,7 +598,8 @@ def test_push_and_pick_and_place_at_config_size(task):
                 assert cls != "bif" or err <= LOOSE[k], (task, s, i, k, err)
                 if cls != "bif":
                     worst[k] = max(worst[k], err)
-    print(task, f"{B} envs, 8 lanes:", {k: f"{v:.1e}" for k, v in worst.items()}, counts)
+    print(task, f"{B} envs, 8 lanes:", {k: f"{v:.1e}" for k, v in worst.items()}, counts,
+          f"terminated {terminated} of {3 * B}; sampled mismatches with the oracle (straddling) {flag_mismatch}")
     assert counts["bif"] <= 0.08 * 3 * len(sample)
 
 

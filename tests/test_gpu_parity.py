@@ -17,6 +17,7 @@ import pytest
 import torch
 
 from helpers import OBJECT_ROWS, oracle_config_for, oracle_env_from, snapshot
+from pandasim._lib import NUM_FLOAT_ROWS as L_ROWS
 
 import oracle as O
 
@@ -25,7 +26,9 @@ pytestmark = pytest.mark.gpu
 ALL_TASKS = ["reach", "push", "pick_and_place", "slide", "stack", "flip"]
 OBJECT_TASKS = ALL_TASKS[1:]
 TASKS = [(t, c) for t in ALL_TASKS for c in ("ee", "joints")]
-FREE_GRIPPER = ("pick_and_place", "stack", "flip")  # panda_tasks.py:26,43,111
+from parity_judge import FREE_GRIPPER, LOOSE, NOISE_K, TOL, done_flags_ok, not_tight_cap
+from parity_judge import groups_for as _groups
+from parity_judge import judge as _judge
 
 
 @pytest.fixture(scope="module")
@@ -270,211 +273,22 @@ def test_sim_step_parity_same_motors(ps, task):
         assert conditioned.mean() <= 0.02
 
 
-# Per-component tolerances of the fused env step (fp32 GPU vs fp64 oracle from
-# the same state).  Reach/Push/Slide measure ~1e-6 m / ~1e-4 m/s.  The tasks
-# with a free gripper (PickAndPlace, Stack, Flip) meet those bounds except on
-# samples at a finger-limit bifurcation: fingers resting exactly at their
-# lower limit (q = 0 after every reset) under a closing command sit at
-# |q| ~ 1e-22, and a joint-limit row exists only while the penetration is
-# <= 0 (btMultiBodyJointLimitConstraint::createConstraintRows skips rows with
-# positive penetration), so on a substep where rounding leaves q > 0 the 170 N
-# finger motor drives the finger ~7 mm past the limit in one substep and the
-# reaction moves the hand.  Which substeps that happens on is decided by
-# rounding: in the fp64 oracle alone a 1e-9 relative change of one joint
-# moves the end effector by 8e-4 m; the same holds at the
-# upper limit (0.04 m) for an opening command.  Such samples are found with
-# the oracle alone: a sample is ill-conditioned when the oracle's own answer
-# moves beyond the tight bound when the state is changed at fp32 resolution
-# (FP32_PROBES: a finger by one fp32 ulp of its range, 4e-9 m, or its
-# velocity by 1e-7 relative; joint 2 by 1e-7 relative) or when 4e-9 m of
-# per-substep noise on the finger positions (one fp32 ulp of their range: the
-# resolution at which the fp32 path places a finger pressed against its limit)
-# is added; those are held to the loose
-# bounds, every other sample to the tight ones (object velocities: atol +
-# 1e-3 relative, _within).
-_TIGHT = dict(ee_pos=2e-5, ee_vel=2e-3, width=2e-4, obj_pos=2e-5, obj_rot=1e-4, obj_vel=1e-4, obj_avel=2e-3)
-_LOOSE = dict(ee_pos=3e-3, ee_vel=2e-1, width=1e-2, obj_pos=1e-3, obj_rot=5e-3, obj_vel=5e-2, obj_avel=2e-1)
-_TIGHT2 = dict(_TIGHT, **{f"obj2_{k[4:]}": v for k, v in _TIGHT.items() if k.startswith("obj_")})
-TOL = {"reach": _TIGHT, "push": _TIGHT, "slide": _TIGHT, "pick_and_place": _TIGHT, "stack": _TIGHT2, "flip": _TIGHT}
-LOOSE = dict(_LOOSE, **{f"obj2_{k[4:]}": v for k, v in _LOOSE.items() if k.startswith("obj_")})
-
-
-def _groups(task, robot_dim):
-    """Observation slices: robot (panda.py:109-119), then the task's object
-    blocks (position, rotation -- a quaternion for Flip --, velocity, angular
-    velocity; Stack has two)."""
-    g = {"ee_pos": [0, 1, 2], "ee_vel": [3, 4, 5]}
-    if robot_dim == 7:
-        g["width"] = [6]
-    k = robot_dim
-    nrot = 4 if task == "flip" else 3
-    for b in range({"reach": 0, "stack": 2}.get(task, 1)):
-        p = "obj_" if b == 0 else "obj2_"
-        g[p + "pos"] = list(range(k, k + 3))
-        g[p + "rot"] = list(range(k + 3, k + 3 + nrot))
-        k += 3 + nrot
-        g[p + "vel"] = list(range(k, k + 3))
-        g[p + "avel"] = list(range(k + 3, k + 6))
-        k += 6
-    return g
-
-
-def _fp32_probes():
-    """State changes at fp32 resolution: each finger's position by one fp32
-    ulp of its range (4e-9 m) and its velocity by 1e-7 relative, either sign;
-    joint 2 by 1e-7 relative; each arm joint by one fp32 ulp of its angle,
-    either sign (an arm joint pressed against its limit by a motor target
-    beyond it flips its limit row like a finger does)."""
-    probes = []
-    for d in (7, 8):
-        for sg in (1.0, -1.0):
-            probes.append(lambda e, d=d, sg=sg: e.q.__setitem__(d, e.q[d] + sg * 4e-9))
-            probes.append(lambda e, d=d, sg=sg: e.qd.__setitem__(d, e.qd[d] * (1 + sg * 1e-7) + sg * 1e-9))
-    probes.append(lambda e: e.q.__setitem__(1, e.q[1] * (1 + 1e-7)))
-    for d in range(7):
-        for sg in (1.0, -1.0):
-            probes.append(lambda e, d=d, sg=sg: e.q.__setitem__(
-                d, float(np.nextafter(np.float32(e.q[d]), np.float32(sg * np.inf)))))
-    return probes
-
-
-FP32_PROBES = _fp32_probes()
-
-
-STEP_DT = 20 / 500  # one env step: 20 substeps of 1/500 s (core.py n_substeps, timestep)
-
-
-def _within(err, o, groups, k, tol, before=None):
-    """err <= tol[k], relative for the object velocities: an impact that spins
-    a cube up to ~30 rad/s within one step -- or stops such a spin: `before`
-    holds the groups' magnitudes at the start of the step -- is resolved by
-    the 50-iteration PGS to ~1e-4 relative, so their bound is atol + 1e-3 x
-    the larger magnitude; an object's rotation accrues that angular-velocity
-    allowance over the step (+ STEP_DT x 1e-3 |omega|)."""
-    before = before or {}
-    bound = tol[k]
-    if k.startswith("obj") and k.endswith(("_vel", "_avel")):
-        bound += 1e-3 * max(np.abs(o[groups[k]]).max(), before.get(k, 0.0))
-    if k.startswith("obj") and k.endswith("_rot"):
-        ka = k[:-4] + "_avel"
-        bound += STEP_DT * 1e-3 * max(np.linalg.norm(o[groups[ka]]), before.get(ka, 0.0))
-    return err <= bound
-
-
-def _before(snap, i, task):
-    """The objects' velocity magnitudes (largest component) at the start of
-    the step, keyed like _groups (for _within)."""
-    out = {}
-    f = snap["f"][:, i]
-    for b, r in enumerate(OBJECT_ROWS[:{"reach": 0, "stack": 2}.get(task, 1)]):
-        p = "obj_" if b == 0 else "obj2_"
-        out[p + "vel"] = float(np.abs(f[r + 7:r + 10]).max())
-        out[p + "avel"] = float(np.abs(f[r + 10:r + 13]).max())
-    return out
-
-
-def _euler_matrix(e):
-    """R = Rz(yaw) Ry(pitch) Rx(roll) of pybullet's getEulerFromQuaternion."""
-    (cr, cp, cy), (sr, sp, sy) = np.cos(e), np.sin(e)
-    return np.array([[cy * cp, cy * sp * sr - sy * cr, cy * sp * cr + sy * sr],
-                     [sy * cp, sy * sp * sr + cy * cr, sy * sp * cr - cy * sr],
-                     [-sp, cp * sr, cp * cr]])
-
-
-def _obs_err(a, b, k, idx, task):
-    """max |a - b| over a group.  Euler angles (every task but Flip, whose
-    rotation is a quaternion) are compared as the angle between the two
-    orientations: +-pi is one orientation, and at pitch +-pi/2 (a cube
-    resting on a side face) roll and yaw are not separately determined."""
-    a, b = np.asarray(a, np.float64)[idx], np.asarray(b, np.float64)[idx]
-    if k.endswith("_rot") and task != "flip":
-        fro = np.linalg.norm(_euler_matrix(a) - _euler_matrix(b))
-        return float(2.0 * np.arcsin(min(fro / (2.0 * np.sqrt(2.0)), 1.0)))
-    return float(np.abs(a - b).max())
-
-
-def _ill_conditioned(cfg, snap, i, action, o_ref, groups, tol, task=""):
-    """True when the oracle's own step from env i of `snap` is not determined
-    to the tight bounds at fp32 resolution: one of FP32_PROBES (the state
-    changed at fp32 resolution) or a per-substep finger-position noise of
-    4e-9 m -- one fp32 ulp of the finger range, the resolution at which the
-    fp32 path places a finger pressed against its limit (oracle.set_finger_noise),
-    or a constant 4e-9 m per-substep offset of the fingers either way
-    (oracle.set_finger_bias: a finger limit row that flips on one substep, e.g.
-    the substep a blocked finger strikes the table) -- moves its observation
-    beyond them."""
-    runs = ([(p, None, 0.0) for p in FP32_PROBES] + [(None, seed, 0.0) for seed in range(4)] +
-            [(None, None, b) for b in (4e-9, -4e-9)])
-    try:
-        for probe, seed, bias in runs:
-            e = oracle_env_from(cfg, snap, i)
-            if probe is not None:
-                probe(e)
-            O.set_finger_noise(4e-9 if seed is not None else 0.0, 0 if seed is None else seed)
-            O.set_finger_bias(bias)
-            o, *_ = O.step(cfg, e, action)
-            if any(not _within(_obs_err(o, o_ref, k, idx, task), o_ref, groups, k, tol, _before(snap, i, task))
-                   for k, idx in groups.items()):
-                return True
-    finally:
-        O.set_finger_noise(0.0)
-        O.set_finger_bias(0.0)
-    return False
-
-
-# Conditioning-scaled bound: a sample beyond the tight bounds is still within
-# them once the oracle's own sensitivity to the fp32 resolution of the state is
-# allowed for -- the largest move of its observation over four runs with
-# NOISE_K fp32 ulps of noise on every state component per substep and one run
-# whose state is rounded to fp32 after every substep (the GPU's state storage;
-# oracle.set_state_noise).  NOISE_K = 2: the fp32 path rounds its arithmetic as
-# well as its state, and the free runs' yardstick uses the same two ulps
-# (tests/test_gpu_contacts.py ULP_NOISE, scripts/free_run_yardstick.py).
-NOISE_K = 2.0
-
-
-def _sensitivity(cfg, snap, i, action, o_ref, groups, task):
-    sens = {k: 0.0 for k in groups}
-    try:
-        for ulps, seed in [(NOISE_K, 1), (NOISE_K, 2), (NOISE_K, 3), (NOISE_K, 4), (-1.0, 0)]:
-            O.set_state_noise(ulps, seed)
-            o, *_ = O.step(cfg, oracle_env_from(cfg, snap, i), action)
-            for k, idx in groups.items():
-                sens[k] = max(sens[k], _obs_err(o, o_ref, k, idx, task))
-    finally:
-        O.set_state_noise(0.0)
-    return sens
-
-
-def _judge(cfg, snap, i, action, o, og, groups, task):
-    """Classifies one teacher-forced sample (GPU observation og vs oracle o):
-    'tight' within the tight bounds; 'conditioned' within them once the
-    oracle's sensitivity (_sensitivity) is added; 'bif' at a branch the oracle itself
-    cannot resolve at fp32 resolution (its answer leaves the tight bounds
-    under the state noise of _sensitivity, or under _ill_conditioned's probes:
-    held to the loose bounds); 'beyond' otherwise.  Returns (class, per-group
-    errors)."""
-    tol = TOL[task]
-    bf = _before(snap, i, task)
-    errs = {k: _obs_err(og, o, k, idx, task) for k, idx in groups.items()}
-    bad = [k for k in groups if not _within(errs[k], o, groups, k, tol, bf)]
-    if not bad:
-        return "tight", errs
-    sens = _sensitivity(cfg, snap, i, action, o, groups, task)
-    if all(_within(errs[k] - sens[k], o, groups, k, tol, bf) for k in bad):
-        return "conditioned", errs
-    # the oracle's own answer leaves the tight bounds under fp32-resolution
-    # state noise (a limit row or contact that flickers on some substeps and
-    # not on others), or under one of the probes
-    if any(not _within(sens[k], o, groups, k, tol, bf) for k in groups) or \
-            _ill_conditioned(cfg, snap, i, action, o, groups, tol, task):
-        return "bif", errs
-    return "beyond", errs
+# The per-sample classifier (tight / conditioned / ill-conditioned / beyond)
+# and its bounds live in tests/parity_judge.py, where the CPU suite checks that
+# it reports deliberate 1-2 % model errors as failures
+# (tests/test_judge_power.py).
 
 
 @pytest.mark.parametrize("task,control,lanes", TASKS_LANES)
 def test_env_step_parity_teacher_forced(ps, task, control, lanes):
-    """Each fused GPU env step vs one oracle env step from the same state."""
+    """Each fused GPU env step vs one oracle env step from the same state,
+    classified by parity_judge.judge.  No sample may be beyond the tight
+    bounds; a blocked gripper (Reach/Push/Slide) may leave at most 0.5 % of
+    them conditioned or ill-conditioned, a free one 8 % ill-conditioned
+    (finger-limit branches) and 2 % conditioned.  Done flags: `terminated` is
+    the reference's rule on the GPU's own achieved goal bit for bit, and
+    differs from the oracle's only where the two achieved goals straddle the
+    threshold (parity_judge.done_flags_ok); `truncated` equal."""
     B, steps = 64, 10
     env = make_env(ps, task, control, B, lanes=lanes)
     assert env.lanes_per_env == lanes
@@ -487,13 +301,15 @@ def test_env_step_parity_teacher_forced(ps, task, control, lanes):
     worst = {k: 0.0 for k in groups}
     worst_bif = {k: 0.0 for k in groups}
     counts = {"tight": 0, "conditioned": 0, "bif": 0, "beyond": 0}
-    beyond = []
+    beyond, flag_bad = [], []
     flag_mismatch = 0
+    G = env.goal_dim
     for s in range(steps):
         snap = snapshot(env.sim)
         a = rng.uniform(-1, 1, size=(B, env.action_dim)).astype(np.float32)
         obs, r, te, tr, _ = env.step(torch.from_numpy(a).cuda())
         og, te, tr = obs["observation"].cpu().numpy(), te.cpu().numpy(), tr.cpu().numpy()
+        agg = obs["achieved_goal"].cpu().numpy()
         for i in range(B):
             e = oracle_env_from(cfg, snap, i)
             o, ag, dg, rr, t_e, t_r = O.step(cfg, e, a[i])
@@ -510,14 +326,22 @@ def test_env_step_parity_teacher_forced(ps, task, control, lanes):
                     np.savez(os.path.join(os.environ["PANDASIM_DUMP_SAMPLES"], f"{task}_{control}_{s}_{i}.npz"),
                              f=snap["f"][:, i], goal=snap["goal"][:, i], action=a[i], gpu_obs=og[i])
             assert t_r == bool(tr[i])
-            flag_mismatch += t_e != bool(te[i])
+            ok, mismatch = done_flags_ok(task, te[i], agg[i], t_e, ag, snap["goal"][:G, i])
+            flag_mismatch += mismatch
+            if not ok:
+                flag_bad.append((s, i, bool(te[i]), t_e))
     print(task, control, f"lanes {lanes}", counts, "worst", {k: f"{v:.2e}" for k, v in worst.items()},
-          "ill-conditioned worst", {k: f"{v:.2e}" for k, v in worst_bif.items()}, "beyond", beyond[:8])
+          "ill-conditioned worst", {k: f"{v:.2e}" for k, v in worst_bif.items()}, "beyond", beyond[:8],
+          f"terminated mismatches (straddling the threshold) {flag_mismatch}")
     assert not beyond
+    assert not flag_bad, flag_bad
     for k, v in worst_bif.items():
         assert v <= LOOSE[k], (k, v)
-    assert counts["bif"] <= 0.08 * B * steps
-    assert flag_mismatch <= 2
+    if task in FREE_GRIPPER:
+        assert counts["bif"] <= not_tight_cap(task) * B * steps
+        assert counts["conditioned"] <= 0.02 * B * steps
+    else:
+        assert counts["bif"] + counts["conditioned"] <= not_tight_cap(task) * B * steps
 
 
 def test_reach_free_running_parity(ps):
@@ -756,12 +580,15 @@ GROUP_TASKS = [(t, c) for t, c in TASKS if t != "stack"]
 @pytest.mark.parametrize("task,control", GROUP_TASKS)
 def test_group_kernels_match_one_lane(ps, task, control):
     """The 16- and 8-lane group kernels against the one-lane kernel over the
-    same step from the same reset: the joint state of every env equal, bit for
-    bit, the rest to rounding.  They run the same rows in the same order and, built with the same
+    same step from the same reset (no gripper contact yet): the robot's rows
+    (q, qd: rows 0-17) of every env equal bit for bit, every other row within
+    1e-4 (the object's ground rows sum J.v over the group's lanes in another
+    order).  They run the same rows in the same order and, built with the same
     flags (-O3), the same arithmetic (profiles/r04b_groups_o3.log: all ten
-    pairs 0.0 apart in q, qd).  Round 3 had to build them at -O1 after a miscompute of
-    the -O3 Slide group kernels (joint velocities off by 6.8e-3 to 2.1e-1,
-    DESIGN.md §12.6); any such recurrence, or codegen drift, fails here."""
+    pairs 0.0 apart in q, qd).  Round 3's -O3 Slide group kernels were off by
+    6.8e-3 to 2.1e-1 rad/s in the joint velocities; any such
+    recurrence, or codegen drift, fails here.  Contact states:
+    test_group_kernels_match_one_lane_in_contact."""
     B = 64
     res = {}
     for lanes in (1, 8, 16):
@@ -781,3 +608,99 @@ def test_group_kernels_match_one_lane(ps, task, control):
         # profiles/r04c_pytest_gpu.log)
         assert np.array_equal(res[lanes][0:18], res[1][0:18]), (lanes, float(diff[0:18].max()))
         assert diff.max() <= 1e-4, (lanes, float(diff.max()))
+
+
+def _contact_policy(env, task):
+    """Drives the end effector into contact: over the object and through it
+    (test_gpu_contacts._push_policy), or for Reach down onto the table, the
+    fingers closing late (free gripper)."""
+    B = env.num_envs
+
+    def policy(s):
+        ee = env.sim.get_link_position("panda", 11).cpu().numpy()
+        if task == "reach":
+            tgt = ee.copy()
+            tgt[:, 2] = -0.05
+        else:
+            obj = env.sim.get_base_position("object").cpu().numpy()
+            tgt = obj + np.array([0.0, 0.0, 0.06 if s < 6 else 0.0])
+            if s >= 6:
+                tgt[:, 0] += 0.05
+        a = np.zeros((B, env.action_dim), np.float32)
+        a[:, :3] = np.clip(10.0 * (tgt - ee), -1, 1)
+        if env.action_dim == 4:
+            a[:, 3] = -1.0 if s >= 8 else 1.0
+        return a
+
+    return policy
+
+
+@pytest.mark.parametrize("task,control", GROUP_TASKS)
+def test_group_kernels_match_one_lane_in_contact(ps, task, control):
+    """As test_group_kernels_match_one_lane, from a mid-rollout state with
+    gripper-object and gripper-table contacts: an
+    ee-control one-lane run pushes into the object (Reach: presses onto the
+    table) for 9 steps; that state is stepped once more by the one-lane, 8-lane
+    and 16-lane kernels with the same action.  Every env without a gripper
+    contact row in the state before or after keeps the robot rows (q, qd)
+    bit for bit.  In the others a gripper contact row's J.v is a group sum in
+    another order than the one-lane solver's, so they round differently and a
+    contact amplifies it (measured: up to 3e-3 rad/s in qd and 4e-2 in the
+    object's velocities after one step, profiles/r05a_pytest_gpu.log); each
+    kernel's step is therefore held against the oracle from the same state, by
+    parity_judge.judge: no sample beyond, and the one-lane kernel's own caps on
+    the other classes."""
+    from helpers import WR_ROW
+
+    B = 64
+    drv = make_env(ps, task, "ee", B, lanes=1)
+    drv.autoreset = False
+    drv.reset(seed=44)
+    policy = _contact_policy(drv, task)
+    for s in range(9):
+        drv.step(torch.from_numpy(policy(s)).cuda())
+    state0 = drv.sim.state.clone()
+    env = make_env(ps, task, control, B, lanes=1)
+    env.autoreset = False
+    env.reset(seed=44)
+    a = np.random.default_rng(9).uniform(-1, 1, size=(B, env.action_dim)).astype(np.float32)
+    if control == "ee":
+        a[:, :3] = policy(9)[:, :3]
+    res, obs = {}, {}
+    for lanes in (1, 8, 16):
+        env.sim.state.copy_(state0)
+        if lanes == 1:
+            snap = snapshot(env.sim)
+        env.sim._call("ps_set_lanes_per_env", env.sim._ctx, lanes)
+        assert env.sim._lib.ps_step_lanes(env.sim._ctx) == lanes
+        env.sim._call("ps_mark_motor_rows_dirty", env.sim._ctx)
+        o, *_ = env.step(torch.from_numpy(a).cuda())
+        res[lanes] = env.sim.f[:, :B].double().cpu().numpy()
+        obs[lanes] = o["observation"].cpu().numpy()
+    contact = (snap["f"][WR_ROW + 4] != 0) | (res[1][WR_ROW + 4] != 0)
+    assert contact.sum() >= 4, int(contact.sum())  # the gripper rows are exercised
+    for lanes in (8, 16):
+        diff = np.abs(res[lanes] - res[1])
+        rob = diff[0:18].max(0)
+        print(f"{task} {control} {lanes} lanes vs 1 in contact ({int(contact.sum())} of {B} envs with gripper "
+              f"contacts): robot rows max {rob.max():.1e} (contact envs), "
+              f"{rob[~contact].max() if (~contact).any() else 0.0:.1e} (others); other rows max "
+              f"{diff[18:].max():.1e}; envs bit-equal in q, qd: {int((rob == 0).sum())}")
+        assert np.array_equal(res[lanes][0:18, ~contact], res[1][0:18, ~contact]), lanes
+    cfg = oracle_config_for(env.sim.cfg)
+    groups = _groups(task, 7 if task in FREE_GRIPPER else 6)
+    counts = {lanes: {"tight": 0, "conditioned": 0, "bif": 0, "beyond": 0} for lanes in (1, 8, 16)}
+    for i in range(B):
+        o, *_ = O.step(cfg, oracle_env_from(cfg, snap, i), a[i])
+        for lanes in (1, 8, 16):
+            cls, errs = _judge(cfg, snap, i, a[i], o, obs[lanes][i], groups, task)
+            counts[lanes][cls] += 1
+            assert cls != "beyond", (lanes, i, errs)
+            assert cls != "bif" or all(v <= LOOSE[k] for k, v in errs.items()), (lanes, i, errs)
+    print(task, control, "in contact, against the oracle:", counts)
+    for lanes in (1, 8, 16):
+        c = counts[lanes]
+        if task in FREE_GRIPPER:
+            assert c["bif"] <= not_tight_cap(task) * B and c["conditioned"] <= 0.05 * B
+        else:
+            assert c["bif"] + c["conditioned"] <= 0.05 * B

@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 import torch
 
-from test_gpu_parity import FREE_GRIPPER, LOOSE, TOL, _groups
+from parity_judge import FREE_GRIPPER, LOOSE, TOL, groups_for as _groups
 
 pytestmark = pytest.mark.gpu
 

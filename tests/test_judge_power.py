@@ -1,0 +1,65 @@
+"""CPU: the parity classifier (tests/parity_judge.judge) has power (VERDICT r04
+weak 1 / item 1).  The "GPU" is the oracle in fp32-like arithmetic
+(tests/judge_power.py); with a deliberate model error of 1-2 % -- the kind of
+error a wrong constant in include/panda_model.h would be -- the teacher-forced
+workloads of the GPU tests must yield 'beyond' samples (the GPU test's
+assertion would fail), and without one they must yield none.
+
+A mutation can only be seen where it moves the observation by more than the
+tight bounds within one step: a 12 % change of btMultiBody's damping (0.04 ->
+0.045) moves a motor-driven arm's end effector by < 2e-5 m per step (the
+POSITION_CONTROL rows overwrite the damped velocity), so on the random
+workload it is invisible to any per-step check at these bounds; it shows where
+an object slides (the scripted push).  profiles/r05_judge_power.jsonl has the
+full scan at 64 envs and the smallest mutation of each kind that is detected
+(scripts/judge_power_scan.py).
+"""
+import pytest
+
+import judge_power as J
+
+B = 16  # envs per workload here; the committed scan uses the GPU tests' 64
+
+
+@pytest.mark.parametrize("task,control,workload", [("push", "ee", "random"), ("reach", "joints", "random"),
+                                                   ("pick_and_place", "ee", "random"), ("push", "ee", "push"),
+                                                   ("slide", "ee", "push")])
+def test_unmutated_fp32_oracle_has_no_beyond_samples(task, control, workload):
+    counts, *_ = J.classify_workload(task, control, workload, "none", B=B)
+    print(task, control, workload, counts)
+    assert counts["beyond"] == 0
+    # a blocked gripper leaves next to nothing untight (parity_judge.NOT_TIGHT_CAP)
+    if task not in ("pick_and_place", "stack", "flip"):
+        assert counts["conditioned"] + counts["bif"] <= 0.005 * sum(counts.values()) + 1
+
+
+@pytest.mark.parametrize("task,control,workload,mutation", [
+    ("reach", "ee", "random", "motor_kp_x1.01"),
+    ("push", "ee", "random", "motor_kp_x1.01"),
+    ("reach", "joints", "random", "motor_kp_x1.01"),
+    ("push", "ee", "push", "cube_mass_x1.02"),
+    ("push", "ee", "push", "cube_friction_0.51"),
+    ("push", "ee", "push", "finger_box_+0.5mm"),
+    ("push", "ee", "push", "link_damping_0.045"),
+    ("pick_and_place", "ee", "push", "cube_mass_x1.02"),
+])
+def test_model_errors_are_beyond(task, control, workload, mutation):
+    """Each mutation yields beyond samples, and most samples whose fp64 effect
+    alone leaves the tight bounds are classified beyond, not absorbed as
+    conditioned or ill-conditioned."""
+    counts, worst, effect, visible = J.classify_workload(task, control, workload, mutation, B=B)
+    print(task, control, workload, mutation, counts, f"samples the mutation moves beyond the tight bounds: {visible}",
+          {k: f"{v:.1e}" for k, v in effect.items()})
+    assert visible > 0
+    assert counts["beyond"] > 0
+    assert counts["beyond"] >= 0.5 * visible
+
+
+def test_damping_error_on_a_motor_driven_arm_is_below_the_bounds():
+    """The undetectable case, stated: on the random Reach workload the damping
+    mutation's own effect stays inside the tight bounds, so every sample is
+    tight -- the classifier is not hiding it, the step does not show it."""
+    counts, worst, effect, visible = J.classify_workload("reach", "ee", "random", "link_damping_0.045", B=B)
+    print(counts, {k: f"{v:.1e}" for k, v in effect.items()})
+    assert visible == 0 and counts["tight"] == sum(counts.values())
+    assert 0 < effect["ee_pos"] < 2e-5
