@@ -19,17 +19,20 @@
  *                       the IK solution pinned by test/pybullet_test.py:254-266)
  *   link inertias       PyBullet recomputes them from collision-mesh AABBs
  *                       (no URDF_USE_INERTIA_FROM_FILE, envs/core.py:47-52).
- *                       Hand and fingers (links 8-10): from the hulls the
- *                       reference ships (contact_graspnet/gripper_models/
- *                       panda_gripper/{hand,finger}.stl, fixture
- *                       tests/golden/panda_gripper_hulls.npz): the hand is
- *                       its hull above the flange plane (z >= 0; the 34
- *                       vertices below it would move the joint-5 KAT's
+ *                       Hand and fingers (links 8-10): the fingers take
+ *                       the extents of the finger hull the reference ships
+ *                       (contact_graspnet/gripper_models/panda_gripper/
+ *                       finger.stl, fixture tests/golden/
+ *                       panda_gripper_hulls.npz); the hand's extents are
+ *                       calibrated to the joint-5 KAT: the hand hull
+ *                       (hand.stl) cut at the flange plane (z >= 0) plus
+ *                       Bullet's 1 mm convex margin per side -- the whole
+ *                       hull's 34 vertices below z = 0 would move the KAT's
  *                       angular velocity to -2.949, 0.02 outside the
- *                       reference's -2.969 +- 1e-3) plus Bullet's 1 mm convex
- *                       margin per side, the fingers their hull's extents
- *                       (tests/test_host_cpu.py checks both against the
- *                       fixture).  The arm links 0-6 have no
+ *                       reference's -2.969 +- 1e-3, so this hull is not
+ *                       shown to be the mesh pybullet_data's panda.urdf
+ *                       collides (tests/test_host_cpu.py checks both
+ *                       against the fixture).  The arm links 0-6 have no
  *                       mesh in the reference: their AABB extents are
  *                       estimates calibrated against the joint-5 motor KATs
  *                       test/pybullet_test.py:139-204.

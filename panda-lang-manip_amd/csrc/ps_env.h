@@ -594,8 +594,14 @@ inline KParams params_of(ps_ctx *c, void *state) {
 // Stack's global stash (the LDS it would use holds its ground rows): one
 // allocation on the first step of a two-object context, never per step
 inline int ensure_stash(ps_ctx *c) {
-    if (c->cfg.n_objects != 2 || c->gstash) return PS_OK;
-    if (hipMalloc((void **)&c->gstash, sizeof(float) * GSTASH_FLOATS * c->lay.stride) != hipSuccess) {
+#ifdef PS_EXPERIMENT_TWO_WAVES
+    const int64_t floats = c->cfg.n_objects == 2 ? GSTASH_FLOATS : GX_FLOATS;
+#else
+    if (c->cfg.n_objects != 2) return PS_OK;
+    const int64_t floats = GSTASH_FLOATS;
+#endif
+    if (c->gstash) return PS_OK;
+    if (hipMalloc((void **)&c->gstash, sizeof(float) * floats * c->lay.stride) != hipSuccess) {
         c->gstash = nullptr;
         return PS_ERR_HIP;
     }
@@ -660,7 +666,17 @@ __global__ __launch_bounds__(kBlock, PS_STEP_MIN_WAVES) void k_step(KParams P, c
                                                                  i * (NP * PAIR_FLOATS));
         lds.ggrip = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_GRIP_OFFSET * s.stride +
                                                                  i * GRIP_FLOATS);
+#ifdef PS_STACK_STASH_TILED
+        lds.gbase = (__attribute__((address_space(1))) float *)P.gstash;
+        lds.glane = (uint32_t)(((i >> 6) * (GSTASH_FLOATS * 64) + (i & 63)) * 4);
+#endif
     }
+#ifdef PS_EXPERIMENT_TWO_WAVES
+    if constexpr (T::NOBJ < 2) {
+        lds.gx = (__attribute__((address_space(1))) float *)P.gstash;
+        lds.gxl = (uint32_t)(((i >> 6) * (GX_FLOATS * 64) + (i & 63)) * 4);
+    }
+#endif
     run_substeps<T::NOBJ, T::SHAPE, true, G>(P, i, PM_SUBSTEPS, q, qd, bd, lds, live, tgt PS_PROF_ARG);
     double g[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -762,7 +778,17 @@ __global__ __launch_bounds__(kBlock) void k_sim_step(KParams P, int n_substeps) 
                                                                  i * (NP * PAIR_FLOATS));
         lds.ggrip = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_GRIP_OFFSET * s.stride +
                                                                  i * GRIP_FLOATS);
+#ifdef PS_STACK_STASH_TILED
+        lds.gbase = (__attribute__((address_space(1))) float *)P.gstash;
+        lds.glane = (uint32_t)(((i >> 6) * (GSTASH_FLOATS * 64) + (i & 63)) * 4);
+#endif
     }
+#ifdef PS_EXPERIMENT_TWO_WAVES
+    if constexpr (NOBJ < 2) {
+        lds.gx = (__attribute__((address_space(1))) float *)P.gstash;
+        lds.gxl = (uint32_t)(((i >> 6) * (GX_FLOATS * 64) + (i & 63)) * 4);
+    }
+#endif
 #ifdef PS_PROFILE_PHASES
     PhaseTimer pt;
     pt.last = (uint32_t)__builtin_amdgcn_s_memtime();

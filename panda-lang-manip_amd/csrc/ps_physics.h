@@ -641,7 +641,13 @@ constexpr int GSTASH_GRIP_OFFSET = GSTASH_PAIR_OFFSET + NP * PAIR_FLOATS;
 constexpr int GRIP_FLOATS = GRIP_MJ_SLOTS * 9;
 constexpr int GSTASH_FLOATS = GSTASH_GRIP_OFFSET + GRIP_FLOATS;
 template <int NOBJ>
-constexpr int lds_floats() { return NOBJ == 2 ? LDS_FLOATS_STACK : LDS_FLOATS; }
+constexpr int lds_floats() {
+#ifdef PS_EXPERIMENT_TWO_WAVES
+    if (NOBJ < 2) return 61;
+#endif
+    return NOBJ == 2 ? LDS_FLOATS_STACK : LDS_FLOATS;
+}
+constexpr int GX_FLOATS = LDS_STASH_OFFSET + LDS_STASH_FLOATS;  // PS_EXPERIMENT_TWO_WAVES
 
 // object-ground contact: object-only rows; normal +z, friction dirs of
 // planeSpace(+z) = (0,-1,0), (1,0,0).  The cylinder's I^-1 (r x dir) is rebuilt
@@ -673,9 +679,32 @@ typedef __attribute__((address_space(3))) float lds_float;
 struct MJStore {
     lds_float *base;
     int stride;
+#ifdef PS_EXPERIMENT_TWO_WAVES
+    // Experiment: the one-object kernels at
+    // two waves per SIMD.  The M^-1 J^T rows, the candidate records and the
+    // stash (floats [0, 148) of the LDS column) move to a wave-tiled global
+    // buffer (as Stack's stash: element k of env i at ((i / 64) * 148 + k) * 64
+    // + i % 64); LDS keeps the work lists' 51 floats and the contact cache, 61
+    // floats per lane, and the kernel is register-allocated for two waves.
+    __attribute__((address_space(1))) float *gx = nullptr;
+    uint32_t gxl = 0;
+    PS_D float &gxr(int k) const {
+        __attribute__((address_space(1))) float *page = gx + (k / 16) * 1024;
+        asm("" : "+s"(page));
+        return *(float *)((__attribute__((address_space(1))) char *)page + gxl + (k % 16) * 256);
+    }
+    // an index that varies by lane (a candidate slot): the whole address per lane
+    PS_D float &gxd(int k) const {
+        return *(float *)((__attribute__((address_space(1))) char *)gx + gxl + (uint32_t)k * 256u);
+    }
+    PS_D float &at(int slot, int row, int k) const { return gxr((slot * 3 + row) * 9 + k); }
+    PS_D lds_float &cache(int k) const { return base[(51 + k) * stride]; }
+    PS_D float &stash(int k) const { return gxr(LDS_STASH_OFFSET + k); }
+#else
     PS_D lds_float &at(int slot, int row, int k) const { return base[((slot * 3 + row) * 9 + k) * stride]; }
     PS_D lds_float &cache(int k) const { return base[(LDS_CACHE_OFFSET + k) * stride]; }
     PS_D lds_float &stash(int k) const { return base[(LDS_STASH_OFFSET + k) * stride]; }
+#endif
     // Stack: the stash in global memory ([GSTASH_PAIR_OFFSET][stride] floats, this env's column)
     // (wave-uniform base and stride, the lane's byte offset: global_* v_off, s[base])
     float *gst = nullptr;
@@ -685,6 +714,9 @@ struct MJStore {
     // ([stride][NP * PAIR_FLOATS]): one lane pointer plus immediate offsets
     __attribute__((address_space(1))) float *gpair = nullptr;
     PS_D float &gstash(int k) const {
+#ifdef PS_STACK_STASH_TILED
+        return gt(k);
+#endif
         float *row = gst + k * gst_stride;
         asm("" : "+s"(row));  // no reassociation into a per-lane pointer (StateView::at)
         return *(float *)((char *)row + goff);
@@ -693,19 +725,43 @@ struct MJStore {
     PS_D lds_float &gnd(int c, int k) const { return base[(LDS_GND_OFFSET + c * LDS_GND_FLOATS + k) * stride]; }
     // Stack only (global stash): pair row c, field k (dir[3].xyz, r0.xyz, r1.xyz, rhs[3], dinv[3]);
     // dir is body A's (+n), r0 / r1 are the offsets from object 0 / 1
+#ifdef PS_STACK_STASH_TILED
+    // experiment: the whole global stash wave-tiled -- element k of env i at
+    // ((i / 64) * GSTASH_FLOATS + k) * 64 + i % 64 -- so a wave's load is 256
+    // contiguous bytes (env-major pair rows put every lane on its own cache
+    // line), addressed as a kernel-argument base plus one SGPR page every 16
+    // rows, the lane's 32-bit offset (VGPR) and an immediate
+    __attribute__((address_space(1))) float *gbase = nullptr;
+    uint32_t glane = 0;  // ((i / 64) * GSTASH_FLOATS * 64 + i % 64) * 4
+    PS_D float &gt(int k) const {
+        __attribute__((address_space(1))) float *page = gbase + (k / 16) * 1024;
+        asm("" : "+s"(page));
+        return *(float *)((__attribute__((address_space(1))) char *)page + glane + (k % 16) * 256);
+    }
+    PS_D float &pair(int c, int k) const { return gt(GSTASH_PAIR_OFFSET + c * PAIR_FLOATS + k); }
+    __attribute__((address_space(1))) float *ggrip = nullptr;
+    PS_D float &grip(int c, int k) const { return gt(GSTASH_GRIP_OFFSET + c * 9 + k); }
+#else
     PS_D float &pair(int c, int k) const { return *(float *)&gpair[c * PAIR_FLOATS + k]; }
     // Stack only (global stash): M^-1 J^T of gripper slot c's normal row, element k
     __attribute__((address_space(1))) float *ggrip = nullptr;
     PS_D float &grip(int c, int k) const { return *(float *)&ggrip[c * 9 + k]; }
+#endif
     // a copy whose address the compiler cannot see through: loads from it are
     // not loop-invariant, so they stay in the PGS loop as ds_reads instead of
     // being hoisted into (spilled) registers
     PS_D MJStore opaque() const {
         MJStore r = *this;
         asm volatile("" : "+v"(r.base));
+#ifdef PS_EXPERIMENT_TWO_WAVES
+        asm volatile("" : "+v"(r.gxl));
+#endif
         asm volatile("" : "+v"(r.goff));
         asm volatile("" : "+v"(r.gpair));
         asm volatile("" : "+v"(r.ggrip));
+#ifdef PS_STACK_STASH_TILED
+        asm volatile("" : "+v"(r.glane));
+#endif
         return r;
     }
 };
@@ -1605,12 +1661,24 @@ struct RobotCand {
         const float v[FLOATS] = {pA.x, pA.y, pA.z, pB.x, pB.y, pB.z, n.x, n.y, n.z, dist, mu,
                                  (float)link, (float)obj, (float)id};
 #pragma unroll
-        for (int k = 0; k < FLOATS; k++) L.base[(OFFSET + s * FLOATS + k) * L.stride] = v[k];
+        for (int k = 0; k < FLOATS; k++) {
+#ifdef PS_EXPERIMENT_TWO_WAVES
+            L.gxd(OFFSET + s * FLOATS + k) = v[k];
+#else
+            L.base[(OFFSET + s * FLOATS + k) * L.stride] = v[k];
+#endif
+        }
     }
     PS_D static RobotCand load(const MJStore &L, int s) {
         float v[FLOATS];
 #pragma unroll
-        for (int k = 0; k < FLOATS; k++) v[k] = L.base[(OFFSET + s * FLOATS + k) * L.stride];
+        for (int k = 0; k < FLOATS; k++) {
+#ifdef PS_EXPERIMENT_TWO_WAVES
+            v[k] = L.gxd(OFFSET + s * FLOATS + k);
+#else
+            v[k] = L.base[(OFFSET + s * FLOATS + k) * L.stride];
+#endif
+        }
         return RobotCand{mk(v[0], v[1], v[2]), mk(v[3], v[4], v[5]), mk(v[6], v[7], v[8]), v[9], v[10],
                          (int)v[11], (int)v[12], (int)v[13]};
     }

@@ -217,13 +217,19 @@ ULP_NOISE = 2.0
 ULP_RUNS = 3
 # Free-run floors (absolute, next to the relative yardstick): fraction of
 # env-steps whose ee/object positions are within 1e-3 m of the oracle, 64 envs
-# x 200 steps, seed 2024.  Measured in profiles/r04j_pytest_gpu_detail.log
-# (Push ee 88.8 %, PickAndPlace ee 74.9 %, Reach joints 97.5 %, Push joints
-# 94.1 %; round 3's sphere pads: 88-99 %), each floor ~3 points under its
-# measurement.  The hull-derived gripper boxes reach the table and the object
-# more often than the pads did, and every contact event is a chance to part.
-FREE_RUN_FLOOR = {("push", "ee"): 0.85, ("pick_and_place", "ee"): 0.72,
-                  ("reach", "joints"): 0.94, ("push", "joints"): 0.91}
+# x 200 steps, seed 2024.  Each floor is the lowest of the CPU yardstick's
+# three oracle runs perturbed by ULP_NOISE fp32 ulps per substep from the same
+# initial states (scripts/free_run_yardstick.py,
+# profiles/r04_free_run_yardstick.jsonl: Push ee 83.3 %, PickAndPlace ee
+# 61.9 %, Reach joints 94.8 %, Push joints 93.2 %) less one point,
+# so it is set by how far two runs that differ only by fp32 rounding part, not
+# by a GPU measurement (round 5: 85.2, 75.9, 97.1, 92.7 %,
+# profiles/r05a_pytest_gpu.log).  Every env that leaves the 1e-3 band does so
+# after a contact event; the hull-derived gripper boxes of round 4 touch the
+# table and the object more often than round 3's sphere pads did, which is the
+# accepted cause of the lower fractions.
+FREE_RUN_FLOOR = {("push", "ee"): 0.82, ("pick_and_place", "ee"): 0.61,
+                  ("reach", "joints"): 0.94, ("push", "joints"): 0.92}
 _RUNS = {}
 
 
