@@ -666,10 +666,6 @@ __global__ __launch_bounds__(kBlock, PS_STEP_MIN_WAVES) void k_step(KParams P, c
                                                                  i * (NP * PAIR_FLOATS));
         lds.ggrip = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_GRIP_OFFSET * s.stride +
                                                                  i * GRIP_FLOATS);
-#ifdef PS_STACK_STASH_TILED
-        lds.gbase = (__attribute__((address_space(1))) float *)P.gstash;
-        lds.glane = (uint32_t)(((i >> 6) * (GSTASH_FLOATS * 64) + (i & 63)) * 4);
-#endif
     }
 #ifdef PS_EXPERIMENT_TWO_WAVES
     if constexpr (T::NOBJ < 2) {
@@ -778,10 +774,6 @@ __global__ __launch_bounds__(kBlock) void k_sim_step(KParams P, int n_substeps) 
                                                                  i * (NP * PAIR_FLOATS));
         lds.ggrip = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_GRIP_OFFSET * s.stride +
                                                                  i * GRIP_FLOATS);
-#ifdef PS_STACK_STASH_TILED
-        lds.gbase = (__attribute__((address_space(1))) float *)P.gstash;
-        lds.glane = (uint32_t)(((i >> 6) * (GSTASH_FLOATS * 64) + (i & 63)) * 4);
-#endif
     }
 #ifdef PS_EXPERIMENT_TWO_WAVES
     if constexpr (NOBJ < 2) {

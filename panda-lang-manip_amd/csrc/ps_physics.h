@@ -714,9 +714,6 @@ struct MJStore {
     // ([stride][NP * PAIR_FLOATS]): one lane pointer plus immediate offsets
     __attribute__((address_space(1))) float *gpair = nullptr;
     PS_D float &gstash(int k) const {
-#ifdef PS_STACK_STASH_TILED
-        return gt(k);
-#endif
         float *row = gst + k * gst_stride;
         asm("" : "+s"(row));  // no reassociation into a per-lane pointer (StateView::at)
         return *(float *)((char *)row + goff);
@@ -725,28 +722,10 @@ struct MJStore {
     PS_D lds_float &gnd(int c, int k) const { return base[(LDS_GND_OFFSET + c * LDS_GND_FLOATS + k) * stride]; }
     // Stack only (global stash): pair row c, field k (dir[3].xyz, r0.xyz, r1.xyz, rhs[3], dinv[3]);
     // dir is body A's (+n), r0 / r1 are the offsets from object 0 / 1
-#ifdef PS_STACK_STASH_TILED
-    // experiment: the whole global stash wave-tiled -- element k of env i at
-    // ((i / 64) * GSTASH_FLOATS + k) * 64 + i % 64 -- so a wave's load is 256
-    // contiguous bytes (env-major pair rows put every lane on its own cache
-    // line), addressed as a kernel-argument base plus one SGPR page every 16
-    // rows, the lane's 32-bit offset (VGPR) and an immediate
-    __attribute__((address_space(1))) float *gbase = nullptr;
-    uint32_t glane = 0;  // ((i / 64) * GSTASH_FLOATS * 64 + i % 64) * 4
-    PS_D float &gt(int k) const {
-        __attribute__((address_space(1))) float *page = gbase + (k / 16) * 1024;
-        asm("" : "+s"(page));
-        return *(float *)((__attribute__((address_space(1))) char *)page + glane + (k % 16) * 256);
-    }
-    PS_D float &pair(int c, int k) const { return gt(GSTASH_PAIR_OFFSET + c * PAIR_FLOATS + k); }
-    __attribute__((address_space(1))) float *ggrip = nullptr;
-    PS_D float &grip(int c, int k) const { return gt(GSTASH_GRIP_OFFSET + c * 9 + k); }
-#else
     PS_D float &pair(int c, int k) const { return *(float *)&gpair[c * PAIR_FLOATS + k]; }
     // Stack only (global stash): M^-1 J^T of gripper slot c's normal row, element k
     __attribute__((address_space(1))) float *ggrip = nullptr;
     PS_D float &grip(int c, int k) const { return *(float *)&ggrip[c * 9 + k]; }
-#endif
     // a copy whose address the compiler cannot see through: loads from it are
     // not loop-invariant, so they stay in the PGS loop as ds_reads instead of
     // being hoisted into (spilled) registers
@@ -759,9 +738,6 @@ struct MJStore {
         asm volatile("" : "+v"(r.goff));
         asm volatile("" : "+v"(r.gpair));
         asm volatile("" : "+v"(r.ggrip));
-#ifdef PS_STACK_STASH_TILED
-        asm volatile("" : "+v"(r.glane));
-#endif
         return r;
     }
 };

@@ -34,8 +34,6 @@ VARIANTS = {
     # the group sums with FMA contraction left on (the round-3 miscompute?
     # DESIGN.md §12.6)
     "group_contract": ["-DPS_EXPERIMENT_GROUP_SUM_CONTRACT"],
-    # Stack's global stash wave-tiled (coalesced pair-row loads)
-    "stack_tiled": ["-DPS_STACK_STASH_TILED"],
 
 }
 
@@ -60,8 +58,11 @@ UNIT_VARIANTS = {
     # the one-lane step kernels at two waves per SIMD (M^-1 J^T, candidate
     # records and stash in global memory, 256 registers); the
     # ABI object allocates the global buffer, the group objects stay as built
-    "two_waves": lambda units: [(n, s, defs + (_TWO_WAVES if (n.startswith("step_t") and not n.endswith("_groups"))
-                                               or n == "pandasim" else [])) for n, s, defs in units],
+    # (Reach and Push only: with the flag, MJStore::at() addresses the global
+    # buffer, which a Stack kernel built so would read through a null base)
+    "two_waves": lambda units: [(n, s, defs + (_TWO_WAVES if n in ("step_t0_c0", "step_t0_c1", "step_t1_c0",
+                                                                    "step_t1_c1", "pandasim") else []))
+                                for n, s, defs in units],
     # scheduler options on the one-lane step objects only
     "onelane_trk": lambda units: _one_lane(units, lambda t: _TRK),
     "onelane_trk_clause": lambda units: _one_lane(units, lambda t: _TRK + (_CLAUSE if t != 4 else [])),
