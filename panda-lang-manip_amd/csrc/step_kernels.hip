@@ -3,8 +3,8 @@
 // -DPS_STEP_CONTROL=c (pandasim/build.py), so the pairs compile as parallel
 // jobs.  ps_step (pandasim.hip) calls the pair's launcher.  The one-lane
 // kernel and the launcher form one object; the 16- and 8-lane group kernels
-// form a second (-DPS_STEP_GROUPS=1), which build.py compiles at -O1
-// (DESIGN.md §12.6).
+// form a second (-DPS_STEP_GROUPS=1), compiled with the same flags (-O3;
+// DESIGN.md §12.6).
 #include "ps_env.h"
 
 #if !defined(PS_STEP_TASK) || !defined(PS_STEP_CONTROL)

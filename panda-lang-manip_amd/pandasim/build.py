@@ -8,10 +8,11 @@ of each scene (sim_kernels.hip, 4 objects).
 
 Every object is compiled with the same flags (-O3, no -mllvm scheduler
 options).  Round 3 built the group kernels at -O1 after an -O2/-O3 miscompute
-of Slide's; in round 4's code the -O3 group kernels are bit
-for bit the one-lane kernels (profiles/r04b_groups_o3.log), and
-tests/test_gpu_parity.py::test_group_kernels_match_one_lane requires exactly
-that, so a recurrence fails the GPU tests.  The scheduler options of round 3
+of Slide's; since round 4 the -O3 group kernels keep the
+one-lane kernels' robot rows bit for bit from a reset
+(tests/test_gpu_parity.py::test_group_kernels_match_one_lane) and pass the
+oracle from contact states (test_group_kernels_match_one_lane_in_contact), so
+a recurrence fails the GPU tests.  The scheduler options of round 3
 gained < 2 % in two interleaved runs (profiles/r04b_ab.log) and one of them
 (-amdgpu-use-amdgpu-trackers) made this clang crash intermittently; none is
 kept.

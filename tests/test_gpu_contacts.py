@@ -386,7 +386,10 @@ def test_free_running_200_steps(task, control):
 # configuration the run reaches shows as a step error, where a free run only
 # shows chaos.  Bounds are test_gpu_parity's per-step ones.
 LONG_TF_CASES = [("reach", "joints"), ("push", "ee"), ("push", "joints"), ("pick_and_place", "ee"), ("slide", "ee"),
-                 ("stack", "ee"), ("flip", "ee")]
+                 ("stack", "ee"), ("flip", "ee"),
+                 # round 5: joint control of the other scenes, and a free gripper
+                 # under random gripper actions (finger-limit branches included)
+                 ("slide", "joints"), ("stack", "joints"), ("pick_and_place", "ee-random-gripper")]
 FREE_GRIPPER_TASKS = ("pick_and_place", "stack", "flip")
 
 
@@ -401,17 +404,21 @@ def test_teacher_forced_200_steps(task, control):
     a branch the oracle cannot resolve at that resolution), none the loose ones.
     The free-gripper runs (PickAndPlace, Stack, Flip) hold the gripper half
     open (action 0), as in the event-onset test, so the finger-limit
-    bifurcations stay out."""
+    bifurcations stay out; the "ee-random-gripper" case keeps
+    the random gripper action, so those branches are in, held to the 10-step
+    test's free-gripper caps (8 % ill-conditioned, 2 % conditioned)."""
     from parity_judge import LOOSE, groups_for as _groups, judge as _judge
 
     B, T = 64, 200
+    random_gripper = control == "ee-random-gripper"
+    control = "ee" if random_gripper else control
     env = make_env(task, control, B)
     env.reset(seed=2024)
-    free = task in FREE_GRIPPER_TASKS
+    free = task in FREE_GRIPPER_TASKS and not random_gripper
     if free:
         env.sim.f[7:9, :B] = 0.02
     cfg = oracle_config_for(env.sim.cfg)
-    groups = _groups(task, 7 if free else 6)
+    groups = _groups(task, 7 if task in FREE_GRIPPER_TASKS else 6)
     rng = np.random.default_rng(2024)
     out = os.path.join("gpurun_out", "tf200")
     os.makedirs(out, exist_ok=True)
@@ -443,12 +450,15 @@ def test_teacher_forced_200_steps(task, control):
                     np.savez(os.path.join(out, f"{task}_{control}_{s}_{i}.npz"), f=snap["f"][:, i],
                              goal=snap["goal"][:, i], rng=snap["rng"][:, i], elapsed=snap["elapsed"][i], action=a[i],
                              gpu_obs=og[i], gpu_f_after=after[:, i], oracle_obs=o)
-    print(task, control, counts, "worst (not ill-conditioned)", {k: f"{v:.2e}" for k, v in worst.items()},
-          "beyond:", beyond[:20])
+    print(task, control + (" (random gripper)" if random_gripper else ""), counts, "worst (not ill-conditioned)",
+          {k: f"{v:.2e}" for k, v in worst.items()}, "beyond:", beyond[:20])
     assert counts["beyond"] <= 0.001 * B * T
-    # measured at most 14 conditioned + 3 ill-conditioned of 12 800 (Push ee,
-    # profiles/r04p_pytest_gpu.log); ADVICE r04: cap them near that rate
-    assert counts["conditioned"] + counts["bif"] <= 0.0025 * B * T
+    if random_gripper:
+        assert counts["bif"] <= 0.08 * B * T and counts["conditioned"] <= 0.02 * B * T
+    else:
+        # measured at most 14 conditioned + 3 ill-conditioned of 12 800 (Push ee,
+        # profiles/r04p_pytest_gpu.log); ADVICE r04: cap them near that rate
+        assert counts["conditioned"] + counts["bif"] <= 0.0025 * B * T
 
 
 def test_event_onset_parity_at_bench_config():
