@@ -656,8 +656,13 @@ __global__ __launch_bounds__(kBlock, PS_STEP_MIN_WAVES) void k_step(KParams P, c
         for (int d = 0; d < 9; d++) tgt[d] = m.target[d];
     }
     PS_PHASE(6);
-    __shared__ float smem[lds_floats<T::NOBJ>() * kBlock];
-    MJStore lds{(lds_float *)(smem + threadIdx.x), kBlock};
+    // LDS columns: one per lane, or one per env when the group's lanes share it
+    // (shared_lds<G>, then the work lists' per-lane output rows after them)
+    constexpr bool SHARED = shared_lds<G>();
+    constexpr int NCOL = SHARED ? kBlock / G : kBlock;
+    __shared__ float smem[lds_floats<T::NOBJ>() * NCOL + (SHARED ? CW_OUT_FLOATS * kBlock : 0)];
+    MJStore lds{(lds_float *)(smem + (SHARED ? threadIdx.x / G : threadIdx.x)), NCOL};
+    lds.cwo = SHARED ? (lds_float *)(smem + lds_floats<T::NOBJ>() * NCOL + threadIdx.x) : lds.base + CW_OUT * kBlock;
     if constexpr (T::NOBJ == 2) {
         lds.gst = P.gstash;
         lds.gst_stride = s.stride;
@@ -766,6 +771,7 @@ __global__ __launch_bounds__(kBlock) void k_sim_step(KParams P, int n_substeps) 
     for (int b = 0; b < NOBJ; b++) load_body(s, i, b, bd[b]);
     __shared__ float smem[lds_floats<NOBJ>() * kBlock];
     MJStore lds{(lds_float *)(smem + threadIdx.x), kBlock};
+    lds.cwo = lds.base + CW_OUT * kBlock;
     if constexpr (NOBJ == 2) {
         lds.gst = P.gstash;
         lds.gst_stride = s.stride;

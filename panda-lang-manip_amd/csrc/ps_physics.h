@@ -679,6 +679,10 @@ typedef __attribute__((address_space(3))) float lds_float;
 struct MJStore {
     lds_float *base;
     int stride;
+    // the work lists' per-lane output rows (robot_candidates), stride kBlock:
+    // in this lane's column (base + CW_OUT rows) unless the env's column is
+    // shared by its group's lanes (shared_lds<G>)
+    lds_float *cwo = nullptr;
 #ifdef PS_EXPERIMENT_TWO_WAVES
     // Experiment: the one-object kernels at
     // two waves per SIMD.  The M^-1 J^T rows, the candidate records and the
@@ -1688,7 +1692,19 @@ PS_D int nth_set_bit(uint64_t m, int j) {
 // Scratch: floats [0, 51) of each column, below the RobotCand records.
 constexpr int CW_IN = 0;    // owner: hR (9), box centres (3 x 3), object position (3), rotation (9)
 constexpr int CW_OUT = 30;  // worker: pick 0 (pA, pB, n, dist), pick 1, count
-static_assert(CW_OUT + 21 <= RobotCand::OFFSET, "work-list scratch below the candidate records");
+constexpr int CW_OUT_FLOATS = 21;
+static_assert(CW_OUT + CW_OUT_FLOATS <= RobotCand::OFFSET, "work-list scratch below the candidate records");
+
+// The group kernels (G > 1) keep one LDS column per env, shared by the
+// group's lanes: every lane of a group computes the same values, so the
+// M^-1 J^T rows, candidate records, stash and cache are written with the same
+// bits by each (round 5; round 3's attempt at this changed the bits, most
+// likely through the FMA-contracted group sums of §12.8, since fixed).  The
+// work lists' outputs, which differ per lane, keep a per-lane area.  LDS per
+// workgroup 40.4 KB -> 7.9 KB (G = 16) / 10.4 KB (G = 8); C3 and C4 0.6 %
+// faster.
+template <int G>
+constexpr bool shared_lds() { return G > 1; }
 
 template <int NOBJ, int SHAPE, int G>
 PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const M3 *oR, const MJStore &lds PS_PROF_PARAM) {
@@ -1706,8 +1722,13 @@ PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const
     // G > 1: every lane of a group holds the same env; its first lane owns the pairs
     const uint32_t leader = lane & ~(uint32_t)(G - 1);
     const uint64_t below = (1ull << leader) - 1ull;
-    lds_float *const col0 = lds.base - lane;  // column 0 of the wave's LDS block
-    auto at = [&](int k, int c) -> lds_float & { return col0[k * lds.stride + c]; };
+    constexpr bool SHARED = shared_lds<G>();
+    // column 0 of the wave's LDS block; lane c's column (its env's when shared)
+    lds_float *const col0 = lds.base - (SHARED ? lane / G : lane);
+    auto at = [&](int k, int c) -> lds_float & { return col0[k * lds.stride + (SHARED ? c / G : c)]; };
+    // worker lane c's output row q (stride kBlock: 64 lanes)
+    lds_float *const cwo0 = lds.cwo - lane;
+    auto wout = [&](int q, int c) -> lds_float & { return cwo0[q * 64 + c]; };
     static_for<0, NOBJ + 1>([&](auto TT) {
         constexpr int TGT = decltype(TT)::value == NOBJ ? 2 : decltype(TT)::value;
         constexpr bool GROUND = TGT == 2;
@@ -1818,8 +1839,8 @@ PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const
                     const int nout = GROUND && PM_BOX_GROUND_CONTACTS < 2 ? 10 : 20;
 #pragma unroll
                     for (int q = 0; q < 20; q++)
-                        if (q < nout) lds.base[(CW_OUT + q) * lds.stride] = out[q];
-                    lds.base[(CW_OUT + 20) * lds.stride] = out[20];
+                        if (q < nout) lds.cwo[q * 64] = out[q];
+                    lds.cwo[20 * 64] = out[20];
                 }
                 __syncthreads();
                 // the owners take their pairs of this round, in box order
@@ -1829,17 +1850,17 @@ PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const
                     const int idx = pre[B] + __builtin_popcountll(m[B] & below) - r;
                     if (nearb[B] && idx >= 0 && idx < nact) {
                         const int wl = nth_set_bit(act, idx);
-                        const int ns = (int)at(CW_OUT + 20, wl);
+                        const int ns = (int)wout(20, wl);
                         const float mu = (float)bx.mu * (GROUND ? (float)PM_DEFAULT_FRICTION : sc.fric);
                         const int obj = GROUND ? -1 : TGT;
 #pragma unroll
                         for (int c = 0; c < 2; c++) {
                             if (nr < NR && ns > c) {
-                                const int o = CW_OUT + 10 * c;
-                                offer(RobotCand{mk(at(o, wl), at(o + 1, wl), at(o + 2, wl)),
-                                                mk(at(o + 3, wl), at(o + 4, wl), at(o + 5, wl)),
-                                                mk(at(o + 6, wl), at(o + 7, wl), at(o + 8, wl)), at(o + 9, wl), mu, bx.link,
-                                                obj, 1 + c + (B * 3 + TGT) * 2});
+                                const int o = 10 * c;
+                                offer(RobotCand{mk(wout(o, wl), wout(o + 1, wl), wout(o + 2, wl)),
+                                                mk(wout(o + 3, wl), wout(o + 4, wl), wout(o + 5, wl)),
+                                                mk(wout(o + 6, wl), wout(o + 7, wl), wout(o + 8, wl)), wout(o + 9, wl), mu,
+                                                bx.link, obj, 1 + c + (B * 3 + TGT) * 2});
                             }
                         }
                     }

@@ -55,6 +55,10 @@ def _one_lane(units, flags_of_task):
 _TWO_WAVES = ["-DPS_EXPERIMENT_TWO_WAVES", "-DPS_STEP_MIN_WAVES=2"]
 
 UNIT_VARIANTS = {
+    # the group kernels (one LDS column per env since round 5) register-allocated
+    # for two waves per SIMD
+    "groups_2w": lambda units: [(n, s, defs + (["-DPS_STEP_MIN_WAVES=2"] if n.endswith("_groups") else []))
+                                for n, s, defs in units],
     # the one-lane step kernels at two waves per SIMD (M^-1 J^T, candidate
     # records and stash in global memory, 256 registers); the
     # ABI object allocates the global buffer, the group objects stay as built
