@@ -25,7 +25,7 @@ import ctypes
 import numpy as np
 
 import oracle as O
-from helpers import OBJECT_ROWS, WG_ROWS, WP_ROW, WPN_ROW, WPPT_ROW, WR_ROW, oracle_config_for, oracle_env_from
+from helpers import OBJECT_ROWS, WG_ROWS, WP_ROW, WPN_ROW, WPPT_ROW, WR_ROW, oracle_env_from
 from parity_judge import FREE_GRIPPER, TOL, _before, _obs_err, _within, groups_for, judge
 
 N_ROWS = 121
@@ -174,4 +174,4 @@ def classify_workload(task, control, workload, mutation_name, B=64, steps=None, 
     return counts, worst, effect, visible
 
 
-__all__ = ["MUTATIONS", "classify_workload", "snapshot_of", "oracle_config_for"]
+__all__ = ["MUTATIONS", "classify_workload", "snapshot_of"]
