@@ -80,6 +80,12 @@ PS_HD V3 operator*(float s, V3 a) { return V3{a.x * s, a.y * s, a.z * s}; }
 PS_HD float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 PS_HD V3 cross(V3 a, V3 b) { return V3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
 PS_D float norm(V3 a) { return sqrtf(dot(a, a)); }
+// v_sqrt_f32 / v_rcp_f32 alone (1 ulp): sqrtf and '/' expand to correctly
+// rounded sequences of ~13 and ~10 VALU instructions; the contact candidate
+// streams (Slide's box-cylinder: ~80 of them per pair) use these
+PS_D float fast_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+PS_D float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+PS_D float fast_norm(V3 a) { return fast_sqrt(dot(a, a)); }
 // c + a * s with one fma per component
 PS_HD V3 fma3(V3 a, float s, V3 c) { return V3{fmaf(a.x, s, c.x), fmaf(a.y, s, c.y), fmaf(a.z, s, c.z)}; }
 

@@ -291,8 +291,10 @@ PS_D void bias_forces(const float q[9], const float qd[9], float h[9]) {
 
 // M = L L^T, then M^-1 (packed symmetric) = L^-T L^-1
 PS_D void spd_inverse(float M[45]) {
-    // Cholesky with one reciprocal per column: the 36 off-diagonal divisions
-    // are products with it (an IEEE division is ~10 VALU instructions)
+    // Cholesky with one reciprocal square root per column (v_rsq_f32, 1 ulp:
+    // sqrtf and the IEEE division took ~22 VALU instructions per pivot): the
+    // 36 off-diagonal divisions are products with it, and the inverse below
+    // reads the pivots' reciprocals only
     float L[45], invd[9];
 #pragma unroll
     for (int i = 0; i < 9; i++) {
@@ -302,8 +304,7 @@ PS_D void spd_inverse(float M[45]) {
 #pragma unroll
             for (int q = 0; q < j; q++) s -= L[sidx(i, q)] * L[sidx(j, q)];
             if (i == j) {
-                L[sidx(i, i)] = sqrtf(s);
-                invd[i] = 1.0f / L[sidx(i, i)];
+                invd[i] = __builtin_amdgcn_rsqf(s);  // M is SPD: s > 0
             } else {
                 L[sidx(i, j)] = s * invd[j];
             }
@@ -540,19 +541,20 @@ PS_D float object_closest(const Scene &sc, V3 loc, V3 &cl, V3 &nl) {
     const V3 h = sc.half;
     if constexpr (SHAPE == SHAPE_CYL) {
         float r = h.x, hh = h.z;
-        float rho = sqrtf(loc.x * loc.x + loc.y * loc.y);
+        float rho = fast_sqrt(loc.x * loc.x + loc.y * loc.y);
         float zc = fminf(fmaxf(loc.z, -hh), hh);
-        float s = rho > r ? r / rho : 1.0f;
+        float irho = fast_rcp(rho);  // used only where rho > 1e-12
+        float s = rho > r ? r * irho : 1.0f;
         cl = mk(loc.x * s, loc.y * s, zc);
         V3 dif = loc - cl;
-        float dn = norm(dif);
+        float dn = fast_norm(dif);
         if (dn > 1e-9f) {
-            nl = dif * (1.0f / dn);
+            nl = dif * fast_rcp(dn);
             return dn;
         }
         float side = r - rho, cap = hh - fabsf(loc.z);
         if (side < cap) {
-            nl = rho > 1e-12f ? mk(loc.x / rho, loc.y / rho, 0.0f) : mk(1.0f, 0.0f, 0.0f);
+            nl = rho > 1e-12f ? mk(loc.x * irho, loc.y * irho, 0.0f) : mk(1.0f, 0.0f, 0.0f);
             cl = mk(nl.x * r, nl.y * r, cl.z);
             return -side;
         }
@@ -1020,11 +1022,10 @@ struct BoxCyl {
             bR.m[6 + a] = lc.z;
         }
     }
+    // the candidate stream in the cylinder's frame: emit(ok, robot point,
+    // cylinder point, normal, distance)
     template <class F>
-    PS_D void visit(const Scene &sc, F &&f) const {
-        auto emit = [&](bool ok, V3 lA, V3 lB, V3 ln, float dist) {
-            f(ok, RCand{yc + mul(yR, lA), yc + mul(yR, lB), mul(yR, ln), dist});
-        };
+    PS_D void visit(const Scene &sc, F &&emit) const {
         // 1. box vertices vs the solid (the loops stay rolled: unrolled, the
         // two visits of the 36 candidates spilled ~300 VGPRs in Slide's kernels)
 #pragma unroll 1
@@ -1048,10 +1049,11 @@ struct BoxCyl {
             const float h1 = comp(xh, a1), h2 = comp(xh, a2);
             const V3 fcen = bc + nf * comp(xh, ax);
             const bool side = fabsf(nf.z) < 0.5f;
-            const float nxy = sqrtf(nf.x * nf.x + nf.y * nf.y);
-            const float inv = side ? r / nxy : 0.0f;
+            const float nxy = fast_sqrt(nf.x * nf.x + nf.y * nf.y);
+            const float inv = side ? r * fast_rcp(nxy) : 0.0f;
             const V3 s0 = mk(-nf.x * inv, -nf.y * inv, 0.0f), d0 = s0 - fcen;
             float lo = -hh, hi = hh;
+            bool empty = false;
             const float K[5][3] = {{dot(d0, t1), t1.z, h1},
                                    {-dot(d0, t1), -t1.z, h1},
                                    {dot(d0, t2), t2.z, h2},
@@ -1060,12 +1062,13 @@ struct BoxCyl {
 #pragma unroll
             for (int k = 0; k < 5; k++) {
                 const float k0 = K[k][0], k1 = K[k][1], lim = K[k][2];
-                const float z = (lim - k0) / k1;
-                if (k1 > 1e-12f) hi = fminf(z, hi);
-                else if (k1 < -1e-12f) lo = fmaxf(z, lo);
-                else if (k0 > lim) { lo = 1.0f; hi = -1.0f; }
+                // (branch-free: z is read only where |k1| > 1e-12)
+                const float z = (lim - k0) * fast_rcp(k1);
+                hi = k1 > 1e-12f ? fminf(z, hi) : hi;
+                lo = k1 < -1e-12f ? fmaxf(z, lo) : lo;
+                empty = empty || (fabsf(k1) <= 1e-12f && k0 > lim);
             }
-            const bool ok = side && lo <= hi;
+            const bool ok = side && !empty && lo <= hi;
 #pragma unroll
             for (int e = 0; e < 2; e++) {
                 const V3 lB = mk(s0.x, s0.y, e ? hi : lo);
@@ -1090,11 +1093,11 @@ struct BoxCyl {
             const V3 lp = tmul(bR, p - bc);
             V3 cl = mk(fminf(fmaxf(lp.x, -xh.x), xh.x), fminf(fmaxf(lp.y, -xh.y), xh.y), fminf(fmaxf(lp.z, -xh.z), xh.z));
             const V3 dif = lp - cl;
-            const float dn = norm(dif);
+            const float dn = fast_norm(dif);
             V3 nb;
             float dist;
             if (dn > 1e-9f) {
-                nb = dif * (1.0f / dn);
+                nb = dif * fast_rcp(dn);
                 dist = dn;
             } else {
                 const float bx = xh.x - fabsf(lp.x), by = xh.y - fabsf(lp.y), bz = xh.z - fabsf(lp.z);
@@ -1109,6 +1112,49 @@ struct BoxCyl {
             }
             emit(true, bc + mul(bR, cl), p, -mul(bR, nb), dist);
         }
+    }
+    PS_D RCand to_world(const RCand &l) const { return RCand{yc + mul(yR, l.pA), yc + mul(yR, l.pB), mul(yR, l.n), l.dist}; }
+    // pick_two's selection in the cylinder's frame: the skew coordinate of a
+    // robot point lA is dot(yc - org, w) + dot(lA, yR^T w), and only the two
+    // picks go to world (per candidate, the world transform was 36 VALU of
+    // the ~80 the generic pick_two spends)
+    PS_D int pick(const Scene &sc, V3 org, V3 w, RCand &c0, RCand &c1) const {
+        const float margin = (float)PM_CONTACT_MARGIN_ROBOT;
+        const RCand none{mk(0, 0, 0), mk(0, 0, 0), mk(0, 0, 1), 1.0f};
+        auto sel = [](bool t, const RCand &a, const RCand &b) {
+            return RCand{t ? a.pA : b.pA, t ? a.pB : b.pB, t ? a.n : b.n, t ? a.dist : b.dist};
+        };
+        const V3 wl = tmul(yR, w);
+        const float k0 = dot(yc - org, w);
+        RCand l0 = none, lmin = none, lmax = none;
+        float s0 = 1e30f, vmin = 1e30f, vmax = -1e30f;
+        visit(sc, [&](bool ok, V3 lA, V3 lB, V3 ln, float dist) {
+            const RCand c{lA, lB, ln, dist};
+            const bool valid = ok && dist < margin;
+            const float sv = k0 + dot(lA, wl);
+            const float sc = valid ? fmaf((float)PM_PICK_SKEW_WEIGHT, sv, dist) : 1e30f;
+            const bool take = sc < s0, tmin = valid && sv < vmin, tmax = valid && sv > vmax;
+            s0 = take ? sc : s0;
+            l0 = sel(take, c, l0);
+            vmin = tmin ? sv : vmin;
+            vmax = tmax ? sv : vmax;
+            lmin = sel(tmin, c, lmin);
+            lmax = sel(tmax, c, lmax);
+        });
+        const bool has0 = s0 < 1e29f;
+        const float sf = k0 + dot(l0.pA, wl);
+        const bool hi = vmax - sf >= sf - vmin;
+        const RCand l1 = sel(hi, lmax, lmin);
+        c0 = has0 ? to_world(l0) : none;
+        c1 = has0 ? to_world(l1) : none;
+        const V3 d = c1.pA - c0.pA;
+        const bool has1 = has0 && dot(d, d) > 1e-8f;  // (0.1 mm)^2: not the same point
+        if (has1 && (hi ? vmax : vmin) < sf) {
+            const RCand t = c0;
+            c0 = c1;
+            c1 = t;
+        }
+        return has0 ? (has1 ? 2 : 1) : 0;
     }
 };
 
@@ -1161,34 +1207,69 @@ struct PairCand {
     bool a0;
 };
 
-PS_D int clip_half(const float *iu, const float *iv, const float *id, int n, int axis, float sign, float lim,
-                   float *ou, float *ov, float *od) {
-    int m = 0;
-    for (int i = 0; i < n; i++) {
-        int j = i + 1 == n ? 0 : i + 1;
-        float ca = sign * (axis == 0 ? iu[i] : iv[i]) - lim, cb = sign * (axis == 0 ? iu[j] : iv[j]) - lim;
-        if (ca <= 0.0f) { ou[m] = iu[i]; ov[m] = iv[i]; od[m] = id[i]; m++; }
-        if ((ca < 0.0f && cb > 0.0f) || (ca > 0.0f && cb < 0.0f)) {
-            float t = ca / (ca - cb);
-            ou[m] = iu[i] + t * (iu[j] - iu[i]);
-            ov[m] = iv[i] + t * (iv[j] - iv[i]);
-            od[m] = id[i] + t * (id[j] - id[i]);
-            m++;
-        }
+// The clipped polygon in registers (round 5): a convex quad cut by four
+// half-planes gains at most one vertex per cut, so 8 compile-time slots hold
+// it, and a vertex goes to its runtime slot m by selects over the slots m can
+// reach at that point.  With arrays indexed by m (the oracle's form) the
+// polygons lived in 384 B of scratch per lane in every Stack kernel.
+struct Poly8 {
+    float u[8], v[8], d[8];
+};
+
+// write (u, v, d) to slot m when c; S = the slots m can address
+template <int S>
+PS_D void poly_put(Poly8 &p, int m, bool c, float u, float v, float d) {
+#pragma unroll
+    for (int s = 0; s < S; s++) {
+        const bool w = c && m == s;
+        p.u[s] = w ? u : p.u[s];
+        p.v[s] = w ? v : p.v[s];
+        p.d[s] = w ? d : p.d[s];
     }
-    return m;
+}
+
+// one Sutherland-Hodgman pass (oracle clip_half): keeps sign * coord <= lim,
+// coord = u (AXIS 0) or v (AXIS 1); the input has n <= NI vertices.  Vertex i
+// emits itself and/or the edge crossing, so before its writes m <= 2i and
+// 2i + 1; a count past the NI + 1 slots (rounding at a degenerate edge) drops
+// the extra vertices.
+template <int NI, int AXIS>
+PS_D int clip_half(const Poly8 &in, int n, float sign, float lim, Poly8 &out) {
+    constexpr int NO = NI + 1 < 8 ? NI + 1 : 8;
+    int m = 0;
+    static_for<0, NI>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        constexpr int nx = i + 1 < NI ? i + 1 : 0;
+        const bool act = i < n, wrap = i + 1 >= n;
+        const float au = in.u[i], av = in.v[i], ad = in.d[i];
+        const float bu = wrap ? in.u[0] : in.u[nx], bv = wrap ? in.v[0] : in.v[nx], bd = wrap ? in.d[0] : in.d[nx];
+        const float ca = sign * (AXIS == 0 ? au : av) - lim, cb = sign * (AXIS == 0 ? bu : bv) - lim;
+        const bool keep = act && ca <= 0.0f;
+        poly_put<(2 * i + 1 < NO ? 2 * i + 1 : NO)>(out, m, keep, au, av, ad);
+        m += keep ? 1 : 0;
+        const bool cross = act && ((ca < 0.0f && cb > 0.0f) || (ca > 0.0f && cb < 0.0f));
+        const float t = ca / (ca - cb);  // read only where the edge crosses
+        poly_put<(2 * i + 2 < NO ? 2 * i + 2 : NO)>(out, m, cross, au + t * (bu - au), av + t * (bv - av),
+                                                     ad + t * (bd - ad));
+        m += cross ? 1 : 0;
+    });
+    return m < NO ? m : NO;
 }
 
 PS_D int box_box(const Scene &sc, const Body &b0, const Body &b1, const M3 &R0, const M3 &R1, PairCand out[NP]) {
-    const float h[3] = {sc.half.x, sc.half.y, sc.half.z};
+    const V3 hv = sc.half;
+    const float h[3] = {hv.x, hv.y, hv.z};  // constant indices only
     V3 d = b1.pos - b0.pos;
     float best = 1e30f;
     V3 nref = mk(0, 0, 0);
     int ref = 0, axn = 0;
+#pragma unroll
     for (int b = 0; b < 2; b++)
+#pragma unroll
         for (int ax = 0; ax < 3; ax++) {
             V3 L = col(b == 0 ? R0 : R1, ax);
             float ra = 0.0f, rb = 0.0f;
+#pragma unroll
             for (int k = 0; k < 3; k++) {
                 ra += h[k] * fabsf(dot(col(R0, k), L));
                 rb += h[k] * fabsf(dot(col(R1, k), L));
@@ -1204,47 +1285,68 @@ PS_D int box_box(const Scene &sc, const Body &b0, const Body &b1, const M3 &R0, 
                 nref = L * sg;
             }
         }
-    const M3 &Rr = ref == 0 ? R0 : R1;
-    const M3 &Ri = ref == 0 ? R1 : R0;
+    // reference / incident bodies, selected per element (a select of the
+    // matrices' addresses put them in memory)
+    M3 Rr, Ri;
+#pragma unroll
+    for (int q = 0; q < 9; q++) {
+        Rr.m[q] = ref == 0 ? R0.m[q] : R1.m[q];
+        Ri.m[q] = ref == 0 ? R1.m[q] : R0.m[q];
+    }
     V3 cr = ref == 0 ? b0.pos : b1.pos, ci = ref == 0 ? b1.pos : b0.pos;
     int a1 = axn + 1 == 3 ? 0 : axn + 1, a2 = axn + 2 >= 3 ? axn - 1 : axn + 2;
-    V3 t1 = col(Rr, a1), t2 = col(Rr, a2);
-    V3 cf = cr + nref * h[axn];
+    V3 t1 = colsel(Rr, a1), t2 = colsel(Rr, a2);
+    V3 cf = cr + nref * comp(hv, axn);
     int ai = 0;
     float mostneg = 2.0f, si = 1.0f;
+#pragma unroll
     for (int ax = 0; ax < 3; ax++) {
         float dn = dot(col(Ri, ax), nref);
         if (-fabsf(dn) < mostneg) { mostneg = -fabsf(dn); ai = ax; si = dn > 0.0f ? -1.0f : 1.0f; }
     }
-    int b1i = ai + 1 == 3 ? 0 : ai + 1, b2i = ai + 2 >= 3 ? ai - 1 : ai + 2;
-    float pu[16], pv[16], pd[16], tu[16], tv[16], td[16];
+    int b1i = ai + 1 == 3 ? 0 : ai + 1;
+    Poly8 P{}, T{};
     const float cu[4] = {-1, 1, 1, -1}, cv[4] = {-1, -1, 1, 1};
+#pragma unroll
     for (int k = 0; k < 4; k++) {
+        // the incident face's corner k: axis ai at si h, b1i at cu h, b2i at cv h
         float loc[3];
-        loc[ai] = si * h[ai];
-        loc[b1i] = cu[k] * h[b1i];
-        loc[b2i] = cv[k] * h[b2i];
+#pragma unroll
+        for (int c = 0; c < 3; c++) loc[c] = (c == ai ? si : c == b1i ? cu[k] : cv[k]) * h[c];
         V3 rel = mul(Ri, mk(loc[0], loc[1], loc[2])) + ci - cf;
-        pu[k] = dot(rel, t1);
-        pv[k] = dot(rel, t2);
-        pd[k] = dot(rel, nref);
+        P.u[k] = dot(rel, t1);
+        P.v[k] = dot(rel, t2);
+        P.d[k] = dot(rel, nref);
     }
-    int n = 4;
-    n = clip_half(pu, pv, pd, n, 0, 1.0f, h[a1], tu, tv, td);
-    n = clip_half(tu, tv, td, n, 0, -1.0f, h[a1], pu, pv, pd);
-    n = clip_half(pu, pv, pd, n, 1, 1.0f, h[a2], tu, tv, td);
-    n = clip_half(tu, tv, td, n, 1, -1.0f, h[a2], pu, pv, pd);
+    int n = clip_half<4, 0>(P, 4, 1.0f, comp(hv, a1), T);
+    n = clip_half<5, 0>(T, n, -1.0f, comp(hv, a1), P);
+    n = clip_half<6, 1>(P, n, 1.0f, comp(hv, a2), T);
+    n = clip_half<7, 1>(T, n, -1.0f, comp(hv, a2), P);
+    // the vertices within the margin, in order
+    Poly8 K{};
     int m = 0;
-    for (int k = 0; k < n; k++)
-        if (pd[k] < (float)PM_CONTACT_MARGIN_PAIR) { tu[m] = pu[k]; tv[m] = pv[k]; td[m] = pd[k]; m++; }
+    static_for<0, 8>([&](auto I) {
+        constexpr int k = decltype(I)::value;
+        const bool keep = k < n && P.d[k] < (float)PM_CONTACT_MARGIN_PAIR;
+        poly_put<k + 1>(K, m, keep, P.u[k], P.v[k], P.d[k]);
+        m += keep ? 1 : 0;
+    });
     int take = m < NP ? m : NP;
-    for (int k = 0; k < take; k++) {
+#pragma unroll
+    for (int k = 0; k < NP; k++) {
         int idx = m <= NP ? k : (k * m) / NP;
+        float u = K.u[0], v = K.v[0], dd = K.d[0];
+#pragma unroll
+        for (int s = 1; s < 8; s++) {
+            u = idx == s ? K.u[s] : u;
+            v = idx == s ? K.v[s] : v;
+            dd = idx == s ? K.d[s] : dd;
+        }
         PairCand c;
-        c.pB = cf + t1 * tu[idx] + t2 * tv[idx];
-        c.pA = c.pB + nref * td[idx];
+        c.pB = cf + t1 * u + t2 * v;
+        c.pA = c.pB + nref * dd;
         c.n = nref;
-        c.dist = td[idx];
+        c.dist = dd;
         c.a0 = ref == 1;  // A = incident
         out[k] = c;
     }
@@ -1827,7 +1929,7 @@ PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const
                         for (int q = 0; q < 9; q++) yR.m[q] = at(CW_IN + 21 + q, own);
                         if constexpr (SHAPE == SHAPE_CYL) {
                             const BoxCyl bcy(sc, xc, hR, xh, yc, yR);
-                            ns = pick_two<PM_BOX_CONTACTS>([&](auto &&f) { bcy.visit(sc, f); }, xc, w, c0, c1);
+                            ns = bcy.pick(sc, xc, w, c0, c1);
                         } else {
                             const BoxCube bcu(xc, hR, xh, yc, yR, sc.half);
                             ns = bcu.pick(xc, w, c0, c1);
