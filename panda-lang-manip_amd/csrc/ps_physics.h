@@ -219,8 +219,9 @@ PS_D void link_wrench_f(const Frame &f, V3 w, V3 dw, V3 vo, V3 ao, V3 &F, V3 &N)
     V3 ac = ao + cross(dw, rc) + cross(w, cross(w, rc));
     S3 Iw = rotate_diag(f.R, (float)link_inertia(I, 0), (float)link_inertia(I, 1), (float)link_inertia(I, 2));
     V3 Iww = mul(Iw, w);
-    float cl = (float)PM_LINEAR_DAMPING + (float)PM_LINEAR_DAMPING * norm(vc);
-    float ca = (float)PM_ANGULAR_DAMPING + (float)PM_ANGULAR_DAMPING * norm(w);
+    // (1-ulp square roots: the damping terms are ~1e-4 of the forces)
+    float cl = (float)PM_LINEAR_DAMPING + (float)PM_LINEAR_DAMPING * fast_norm(vc);
+    float ca = (float)PM_ANGULAR_DAMPING + (float)PM_ANGULAR_DAMPING * fast_norm(w);
     F = (ac + vc * cl) * m;
     V3 Nc = mul(Iw, dw) + cross(w, Iww) + Iww * ca;
     N = Nc + cross(c, F);  // about the base origin
@@ -393,7 +394,10 @@ PS_D void inverse_kinematics(const float q_start[9], V3 target, Q4 orn, float q_
                 U[a * (a + 1) / 2 + b] = dot(Jv[a], Jv[b]) + dot(Jw[a], Jw[b]) + (a == b ? (float)PM_IK_DAMPING : 0.0f);
         }
         // Cholesky solve, one reciprocal per pivot (the divisions by it are
-        // products: an IEEE division is ~10 VALU instructions)
+        // products: an IEEE division is ~10 VALU instructions).  A v_rsq_f32
+        // pivot (1 ulp) measured 0.3 % faster per step but, together with the
+        // damping norms' v_sqrt in bias_forces, moved one in-contact Push
+        // sample past the parity bound: not kept.
         float Lc[N * (N + 1) / 2], il[N];
 #pragma unroll
         for (int i = 0; i < N; i++)
@@ -1081,9 +1085,21 @@ struct BoxCyl {
         // palm): a narrower box's face inside a cap is found by its vertices
         constexpr int order[PM_CYL_RIM_POINTS] = PM_CYL_RIM_ORDER;
         constexpr float c45 = 0.70710678118654752f;
-        const int nrim = (xh.x > r || xh.y > r || xh.z > r) ? num_support<SHAPE_CYL>() : 0;
+        // A cap's rim points are skipped by the wave when no lane's box
+        // reaches within the margin (+0.1 mm) of the cap's plane: such points
+        // are farther than the margin from the box, invalid candidates that
+        // cannot change the picks.  The bottom cap lies on the table, out of
+        // the palm's reach, so its 8 points drop out in practically every
+        // wave.  (The range is the wave's, so the loop counter stays scalar.)
+        const bool wide = xh.x > r || xh.y > r || xh.z > r;
+        const float reach = fabsf(bR.m[6]) * xh.x + fabsf(bR.m[7]) * xh.y + fabsf(bR.m[8]) * xh.z +
+                            (float)PM_CONTACT_MARGIN_ROBOT + 1e-4f;
+        const bool cap_lo = wide && fabsf(bc.z + hh) <= reach, cap_hi = wide && fabsf(bc.z - hh) <= reach;
+        const bool any_lo = __builtin_amdgcn_ballot_w64(cap_lo) != 0, any_hi = __builtin_amdgcn_ballot_w64(cap_hi) != 0;
+        const int vbeg = any_lo ? 0 : PM_CYL_RIM_POINTS, vend = any_hi ? 2 * PM_CYL_RIM_POINTS : PM_CYL_RIM_POINTS;
+        static_assert(2 * PM_CYL_RIM_POINTS == num_support<SHAPE_CYL>(), "rim points: bottom cap, then top");
 #pragma unroll 1
-        for (int V = 0; V < nrim; V++) {
+        for (int V = vbeg; V < vend; V++) {
             int j = 0;
 #pragma unroll
             for (int k = 0; k < PM_CYL_RIM_POINTS; k++) j = (V % PM_CYL_RIM_POINTS) == k ? order[k] : j;
@@ -1110,7 +1126,7 @@ struct BoxCyl {
                 cl = ax == 0 ? mk(s * xh.x, cl.y, cl.z) : (ax == 1 ? mk(cl.x, s * xh.y, cl.z) : mk(cl.x, cl.y, s * xh.z));
                 dist = -bst;
             }
-            emit(true, bc + mul(bR, cl), p, -mul(bR, nb), dist);
+            emit(wide, bc + mul(bR, cl), p, -mul(bR, nb), dist);
         }
     }
     PS_D RCand to_world(const RCand &l) const { return RCand{yc + mul(yR, l.pA), yc + mul(yR, l.pB), mul(yR, l.n), l.dist}; }
