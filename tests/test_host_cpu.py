@@ -330,3 +330,45 @@ def test_bench_fp32_roofline_without_the_cpu_leg():
     r = bench.fp32_roofline(bench.committed_work_counts("push"), 1, 2.1e7)
     assert 5.0e5 < r["flops_per_env_step"] < 6.5e5
     assert bench.committed_work_counts("no such task") is None
+
+
+def test_rim_point_culling_skips_only_invalid_candidates():
+    """BoxCyl::visit (csrc/ps_physics.h) skips a cap's rim points for a wave
+    when no lane's box reaches within the margin (+0.1 mm) of the cap's plane
+    (DESIGN.md §12.11).  The argument: a point on the plane z = +-hh of the
+    cylinder frame is at least |bc.z -+ hh| - ez from a box whose extent along
+    z is bc.z +- ez, so every such rim point is an invalid candidate (distance
+    >= the margin) and cannot change the picks.  Checked on random poses of
+    the palm and finger boxes around the Slide cylinder, including poses
+    right at the cut-off."""
+    h = _model_header()
+    margin = 0.005
+    assert "#define PM_CONTACT_MARGIN_ROBOT 0.005" in h
+    r, hh = 0.03, 0.015  # PM_SLIDE_OBJECT_SIZE / 2 radius and height: half extents (r, r, hh)
+    rng = np.random.default_rng(5)
+    ang = np.arange(8) * (np.pi / 4)
+    skipped = 0
+    for box in _boxes(h):
+        xh = np.array(box[4:7])
+        for _ in range(4000):
+            q = rng.normal(size=4)
+            q /= np.linalg.norm(q)
+            w, x, y, z = q
+            R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                          [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                          [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+            ez = np.abs(R[2]) @ xh
+            reach = ez + margin + 1e-4
+            bc = rng.uniform(-0.12, 0.12, size=3)
+            if rng.random() < 0.5:  # put the box's face near a cap's plane
+                cap = rng.choice([-1.0, 1.0])
+                bc[2] = cap * hh + rng.choice([-1.0, 1.0]) * (reach + rng.uniform(-2e-3, 2e-3))
+            for cap in (-1.0, 1.0):
+                if abs(bc[2] - cap * hh) <= reach:
+                    continue
+                skipped += 1
+                p = np.stack([r * np.cos(ang), r * np.sin(ang), np.full(8, cap * hh)], 1)
+                lp = (p - bc) @ R  # the points in the box frame
+                dist = np.linalg.norm(lp - np.clip(lp, -xh, xh), axis=1)
+                assert dist.min() >= margin, (box, bc, cap, dist.min())
+    assert skipped > 1000
