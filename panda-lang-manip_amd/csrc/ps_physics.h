@@ -1395,6 +1395,14 @@ constexpr float kResidualAbs = 3.16227766e-4f;
 // 3.18 to 3.14 ms and Reach from 1.47 to 1.44 ms per step at 65 536 envs.
 #define PS_GATE(cond, likely) __builtin_expect(!!(cond), (likely))
 PS_D float row_viol(float dl, float dinv) { return fmaf(-kResidualAbs, dinv, fabsf(dl)); }
+// The solver's running residual max and its impulse clamps: llvm.maximum
+// (v_maximum3_f32) and v_med3_f32.  With fmaxf/fminf (llvm.maxnum/minnum) the
+// IEEE-mode lowering re-canonicalised the running max (v_max x, x, x) at every
+// row: ~30 VALU instructions per Push iteration.  The values are finite (the
+// residual's 1/den is clamped, see kResidualAbs) and lo <= hi, where the
+// results are the same bits.
+PS_D float res_max(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+PS_D float clamp_impulse(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
 PS_D float joint_viol(float dl, float den) { return fmaf(fabsf(dl), den, -kResidualAbs); }
 
 // The warm start's contact cache (state rows PS_F_WG0.. of this env, see
@@ -1621,13 +1629,13 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         constexpr int d = decltype(DD)::value;
         float s = group_bcast<G, d % G>(dvm[d / G]);
         float dl = rhs - dinvj[d] * (sgn * s);
-        float nl = fminf(fmaxf(lam + dl, lo), hi);
+        float nl = clamp_impulse(lam + dl, lo, hi);
         dl = nl - lam;
         lam = nl;
         PS_REC(dl);
 #pragma unroll
         for (int k = 0; k < K; k++) dvm[k] = fmaf(mrow[k][d], sgn * dl, dvm[k]);
-        res = fmaxf(res, joint_viol(dl, midg[d]));
+        res = res_max(res, joint_viol(dl, midg[d]));
     };
     auto limit_row = [&](auto DD) {
         constexpr int d = decltype(DD)::value;
@@ -1648,12 +1656,12 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
     auto normal = [&](auto KL, const float Jm[K], const float Mm[K], float rhs, float dinv, float &lam) {
         float s = group_sum<G>(prod(KL, Jm));
         float dl = rhs - dinv * s;
-        float nl = fminf(fmaxf(lam + dl, 0.0f), (float)PM_CONTACT_UPPER);
+        float nl = clamp_impulse(lam + dl, 0.0f, (float)PM_CONTACT_UPPER);
         dl = nl - lam;
         lam = nl;
         PS_REC(dl);
         apply(KL, Mm, dl);
-        res = fmaxf(res, row_viol(dl, dinv));
+        res = res_max(res, row_viol(dl, dinv));
     };
     auto cone = [&](auto KL, const float J[3][K], const float M[3][K], const float rhs[3], const float dinv[3],
                     float lam[3], float mu) {
@@ -1672,7 +1680,7 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         PS_REC(dlb);
 #pragma unroll
         for (int k = decltype(KL)::value; k < K; k++) dvm[k] = fmaf(M[2][k], dlb, fmaf(M[1][k], dla, dvm[k]));
-        res = fmaxf(res, fmaxf(row_viol(dla, dinv[1]), row_viol(dlb, dinv[2])));
+        res = res_max(res, res_max(row_viol(dla, dinv[1]), row_viol(dlb, dinv[2])));
     };
     // the object's ground normals touch only object DoFs: they commute with
     // the joint rows (robot DoFs only), so they run in the motor rows' block,
@@ -2476,13 +2484,13 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     if constexpr (G == 1) {
     auto joint_row = [&](int d, float sgn, float rhs, float &lam, float lo, float hi) {
         float dl = rhs - dinvj[d] * (sgn * dv[d]);
-        float nl = fminf(fmaxf(lam + dl, lo), hi);
+        float nl = clamp_impulse(lam + dl, lo, hi);
         dl = nl - lam;
         lam = nl;
         float f = sgn * dl;
 #pragma unroll
         for (int a = 0; a < 9; a++) dv[a] += Mi[sidx(a, d)] * f;
-        res = fmaxf(res, joint_viol(dl, Mi[sidx(d, d)]));
+        res = res_max(res, joint_viol(dl, Mi[sidx(d, d)]));
     };
     auto limit_row = [&](int d) {
         if (PS_GATE(gate_lim & (1u << d), 0)) {
@@ -2659,7 +2667,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     }
                     V3 rn = mk(gr.y, -gr.x, 0.0f);  // r x (0,0,1); zero terms dropped below
                     float dl = grhs - gdinv * (rn.x * dw[b].x + rn.y * dw[b].y + dvl[b].z);
-                    float nl = fminf(fmaxf(g.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
+                    float nl = clamp_impulse(g.lam[0] + dl, 0.0f, (float)PM_CONTACT_UPPER);
                     dl = nl - g.lam[0];
                     g.lam[0] = nl;
                     if constexpr (ANISO) {
@@ -2671,7 +2679,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         dw[b].y = fmaf(rn.y, dI, dw[b].y);
                     }
                     dvl[b].z = fmaf(dl, inv_m, dvl[b].z);
-                    res = fmaxf(res, row_viol(dl, gdinv));
+                    res = res_max(res, row_viol(dl, gdinv));
                 }
         }
         if constexpr (NOBJ == 2) {
@@ -2686,11 +2694,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         const V3 rn1 = cross(mk(pf[c][6], pf[c][7], pf[c][8]), d0);
                         float jv = sg * pair_rel(rn0, rn1, d0);
                         float dl = pf[c][9] - pf[c][10] * jv;
-                        float nl = fminf(fmaxf(p.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
+                        float nl = clamp_impulse(p.lam[0] + dl, 0.0f, (float)PM_CONTACT_UPPER);
                         dl = nl - p.lam[0];
                         p.lam[0] = nl;
                         pair_apply(rn0, rn1, d0, sg * dl);
-                        res = fmaxf(res, row_viol(dl, pf[c][10]));
+                        res = res_max(res, row_viol(dl, pf[c][10]));
                     }
             }
         }
@@ -2715,7 +2723,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 float jv = jrow_dot(Jl, dv);
                 if (NOBJ > 0) jv -= dot(r.rn[0], obj_dw(r.o1)) + dot(r.dir[0], obj_dv(r.o1));
                 float dl = r.rhs[0] - r.dinv[0] * jv;
-                float nl = fminf(fmaxf(r.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
+                float nl = clamp_impulse(r.lam[0] + dl, 0.0f, (float)PM_CONTACT_UPPER);
                 dl = nl - r.lam[0];
                 r.lam[0] = nl;
                 if constexpr (NOBJ == 2) {
@@ -2734,7 +2742,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     float iI = r.o1 ? od[NB - 1].iI : od[0].iI;
                     obj_add(r.o1, r.rn[0] * (-dl * iI), r.dir[0] * (-dl * im));
                 }
-                res = fmaxf(res, row_viol(dl, r.dinv[0]));
+                res = res_max(res, row_viol(dl, r.dinv[0]));
             }
         // friction cones (Stack: the pair rows' loads first, as above)
         float pq[NP][16];
@@ -2797,7 +2805,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     }
                     dvl[b].x = fmaf(dlb, inv_m, dvl[b].x);
                     dvl[b].y = fmaf(-dla, inv_m, dvl[b].y);
-                    res = fmaxf(res, fmaxf(row_viol(dla, gdinv1), row_viol(dlb, gdinv2)));
+                    res = res_max(res, res_max(row_viol(dla, gdinv1), row_viol(dlb, gdinv2)));
                 }
         }
         if constexpr (NOBJ == 2) {
@@ -2826,7 +2834,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         p.lam[2] = sb;
                         pair_apply(rn01, rn11, d1, sg * dla);
                         pair_apply(rn02, rn12, d2, sg * dlb);
-                        res = fmaxf(res, fmaxf(row_viol(dla, pq[c][14]), row_viol(dlb, pq[c][15])));
+                        res = res_max(res, res_max(row_viol(dla, pq[c][14]), row_viol(dlb, pq[c][15])));
                     }
             }
         }
@@ -2895,7 +2903,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                                 fmaf(r.dir[2].z, bm, r.dir[1].z * am));
                     obj_add(r.o1, ddw, ddv);
                 }
-                res = fmaxf(res, fmaxf(row_viol(dla, r.dinv[1]), row_viol(dlb, r.dinv[2])));
+                res = res_max(res, res_max(row_viol(dla, r.dinv[1]), row_viol(dlb, r.dinv[2])));
             }
     };
 
@@ -2910,7 +2918,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 GroundContact &g = gc[0][c];
                 const V3 rn = mk(g.r.y, -g.r.x, 0.0f);  // r x (0,0,1)
                 float dl = g.rhs[0] - g.dinv[0] * (rn.x * dw[0].x + rn.y * dw[0].y + dvl[0].z);
-                const float nl = fminf(fmaxf(g.lam[0] + dl, 0.0f), (float)PM_CONTACT_UPPER);
+                const float nl = clamp_impulse(g.lam[0] + dl, 0.0f, (float)PM_CONTACT_UPPER);
                 dl = nl - g.lam[0];
                 g.lam[0] = nl;
                 if constexpr (ANISO) {
@@ -2921,7 +2929,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     dw[0].y = fmaf(rn.y, dI, dw[0].y);
                 }
                 dvl[0].z = fmaf(dl, od[0].inv_m, dvl[0].z);
-                res = fmaxf(res, row_viol(dl, g.dinv[0]));
+                res = res_max(res, row_viol(dl, g.dinv[0]));
             }
         }
     };
