@@ -1395,14 +1395,15 @@ constexpr float kResidualAbs = 3.16227766e-4f;
 // 3.18 to 3.14 ms and Reach from 1.47 to 1.44 ms per step at 65 536 envs.
 #define PS_GATE(cond, likely) __builtin_expect(!!(cond), (likely))
 PS_D float row_viol(float dl, float dinv) { return fmaf(-kResidualAbs, dinv, fabsf(dl)); }
-// The solver's running residual max and its impulse clamps: llvm.maximum
-// (v_maximum3_f32) and v_med3_f32.  With fmaxf/fminf (llvm.maxnum/minnum) the
-// IEEE-mode lowering re-canonicalised the running max (v_max x, x, x) at every
-// row: ~30 VALU instructions per Push iteration.  The values are finite (the
-// residual's 1/den is clamped, see kResidualAbs) and lo <= hi, where the
-// results are the same bits.
+// The solver's running residual max: llvm.maximum (v_maximum3_f32).  With
+// fmaxf (llvm.maxnum) the IEEE-mode lowering re-canonicalised the running max
+// (v_max x, x, x) at every row: ~30 VALU instructions per Push iteration.  The
+// values are finite (the residual's 1/den is clamped, see kResidualAbs), where
+// both give the same bits.  The impulse clamps stay fminf(fmaxf()): as
+// v_med3_f32 (the same bits too) they made Push 0.25 % slower
+// (profiles/r05v_ab.log).
 PS_D float res_max(float a, float b) { return __builtin_elementwise_maximum(a, b); }
-PS_D float clamp_impulse(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
+PS_D float clamp_impulse(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 PS_D float joint_viol(float dl, float den) { return fmaf(fabsf(dl), den, -kResidualAbs); }
 
 // The warm start's contact cache (state rows PS_F_WG0.. of this env, see
