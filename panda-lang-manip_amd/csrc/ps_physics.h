@@ -752,6 +752,28 @@ struct MJStore {
     }
 };
 
+// v += m s for 9-vectors as four v_pk_fma_f32 and one v_fma_f32: the same
+// fused products, element for element, as nine v_fma_f32 (the gripper rows'
+// M^-1 J^T come from LDS as ds_read2 pairs, already in register pairs)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+PS_D void pk_apply(float v[9], const float m[9], float s) {
+#ifdef PS_EXPERIMENT_NO_PK_APPLY
+#pragma unroll
+    for (int a = 0; a < 9; a++) v[a] = fmaf(m[a], s, v[a]);
+    return;
+#endif
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        f32x2 x = {v[2 * k], v[2 * k + 1]};
+        const f32x2 mm = {m[2 * k], m[2 * k + 1]};
+        const f32x2 ss = {s, s};
+        x = __builtin_elementwise_fma(mm, ss, x);
+        v[2 * k] = x.x;
+        v[2 * k + 1] = x.y;
+    }
+    v[8] = fmaf(m[8], s, v[8]);
+}
+
 PS_D float jrow_dot(const float J[9], const float v[9]) {
     float s = 0.0f;
 #pragma unroll
@@ -1476,6 +1498,10 @@ PS_D float cache_lookup(const float lam[4], unsigned pack, unsigned id) {
 // when |f|^2 = m2 exceeds lim^2, else 1.  Raw v_rsq_f32: rsqrtf's denormal
 // rescaling costs three instructions per cone row; m2 is clamped to FLT_MIN
 // instead, so a denormal m2 cannot produce inf (and 0 * inf) there.
+// lim = mu * lam_n takes the normal impulse as it is: every normal row clamps
+// it to [0, upper] (and warm starts are 0.85 x a clamped impulse), so the
+// oracle's max(lam_n, 0) is the identity here and only cost a v_max (plus a
+// canonicalising one) per cone.
 PS_D float cone_scale(float m2, float lim) {
     return m2 > lim * lim ? lim * __builtin_amdgcn_rsqf(fmaxf(m2, 1.17549435e-38f)) : 1.0f;
 }
@@ -1669,7 +1695,7 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         float sa = group_sum<G>(prod(KL, J[1])), sb = group_sum<G>(prod(KL, J[2]));
         float dla = rhs[1] - dinv[1] * sa, dlb = rhs[2] - dinv[2] * sb;
         float a = lam[1] + dla, b = lam[2] + dlb;
-        float lim = mu * fmaxf(lam[0], 0.0f);
+        float lim = mu * lam[0];  // lam[0] >= 0: the normal row's clamp
         float sc = cone_scale(a * a + b * b, lim);
         a *= sc;
         b *= sc;
@@ -2731,8 +2757,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
 #pragma unroll
                     for (int a = 0; a < 9; a++) dv[a] = fmaf(gmj[c][a], dl, dv[a]);
                 } else {
-#pragma unroll
-                    for (int a = 0; a < 9; a++) dv[a] = fmaf(mj[a], dl, dv[a]);
+                    pk_apply(dv, mj, dl);
                 }
                 if constexpr (NOBJ == 1) {
                     // one object: fma straight into its velocity change
@@ -2785,7 +2810,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     float dla = grhs1 - gdinv1 * (r1.x * dw[b].x + r1.z * dw[b].z - dvl[b].y);
                     float dlb = grhs2 - gdinv2 * (r2.y * dw[b].y + r2.z * dw[b].z + dvl[b].x);
                     float sa = g.lam[1] + dla, sb = g.lam[2] + dlb;
-                    float lim = gmu * fmaxf(g.lam[0], 0.0f);
+                    float lim = gmu * g.lam[0];  // >= 0: the normal row's clamp
                     float m2 = sa * sa + sb * sb;
                     // |f| > mu N: project onto the cone (lim * rsq(m2) <= 1 there)
                     float s = cone_scale(m2, lim);
@@ -2824,7 +2849,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         float jb = sg * pair_rel(rn02, rn12, d2);
                         float dla = pq[c][12] - pq[c][14] * ja, dlb = pq[c][13] - pq[c][15] * jb;
                         float sa = p.lam[1] + dla, sb = p.lam[2] + dlb;
-                        float lim = pmu * fmaxf(p.lam[0], 0.0f);
+                        float lim = pmu * p.lam[0];
                         float m2 = sa * sa + sb * sb;
                         float s = cone_scale(m2, lim);
                         sa *= s;
@@ -2865,7 +2890,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 }
                 float dla = r.rhs[1] - r.dinv[1] * ja, dlb = r.rhs[2] - r.dinv[2] * jb;
                 float sa = r.lam[1] + dla, sb = r.lam[2] + dlb;
-                float lim = r.mu * fmaxf(r.lam[0], 0.0f);
+                float lim = r.mu * r.lam[0];  // >= 0: the normal row's clamp
                 float m2 = sa * sa + sb * sb;
                 float s = cone_scale(m2, lim);
                 sa *= s;
@@ -2880,8 +2905,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     for (int a = 0; a < 9; a++) g[a] = fmaf(J2[a], dlb, J1[a] * dla);
                     mi_apply(g);
                 } else {
-#pragma unroll
-                    for (int a = 0; a < 9; a++) dv[a] = fmaf(mj2[a], dlb, fmaf(mj1[a], dla, dv[a]));
+                    pk_apply(dv, mj1, dla);
+                    pk_apply(dv, mj2, dlb);
                 }
                 if constexpr (NOBJ == 1) {
                     if constexpr (ANISO) {
