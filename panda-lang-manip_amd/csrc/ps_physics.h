@@ -774,6 +774,12 @@ PS_D void pk_apply(float v[9], const float m[9], float s) {
     v[8] = fmaf(m[8], s, v[8]);
 }
 
+// fma3 with x and y as one v_pk_fma_f32 (the same bits)
+PS_D V3 pk_fma3(V3 a, float s, V3 c) {
+    const f32x2 xy = __builtin_elementwise_fma((f32x2){a.x, a.y}, (f32x2){s, s}, (f32x2){c.x, c.y});
+    return mk(xy.x, xy.y, fmaf(a.z, s, c.z));
+}
+
 PS_D float jrow_dot(const float J[9], const float v[9]) {
     float s = 0.0f;
 #pragma unroll
@@ -2761,8 +2767,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 }
                 if constexpr (NOBJ == 1) {
                     // one object: fma straight into its velocity change
-                    dw[0] = ANISO ? dw[0] + od[0].inv_inertia(r.rn[0] * -dl) : fma3(r.rn[0], -dl * od[0].iI, dw[0]);
-                    dvl[0] = fma3(r.dir[0], -dl * od[0].inv_m, dvl[0]);
+                    dw[0] = ANISO ? dw[0] + od[0].inv_inertia(r.rn[0] * -dl) : pk_fma3(r.rn[0], -dl * od[0].iI, dw[0]);
+                    dvl[0] = pk_fma3(r.dir[0], -dl * od[0].inv_m, dvl[0]);
                 } else if constexpr (NOBJ == 2) {
                     float im = r.o1 ? od[NB - 1].inv_m : od[0].inv_m;
                     float iI = r.o1 ? od[NB - 1].iI : od[0].iI;
@@ -2805,32 +2811,68 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         gdinv1 = on ? cube_ground_dinv(gr, 1, od[b].iI, inv_m) : 0.0f;
                         gdinv2 = on ? cube_ground_dinv(gr, 2, od[b].iI, inv_m) : 0.0f;
                     }
-                    V3 r1 = mk(gr.z, 0.0f, -gr.x);  // r x (0,-1,0)
-                    V3 r2 = mk(0.0f, gr.z, -gr.y);  // r x (1,0,0)
-                    float dla = grhs1 - gdinv1 * (r1.x * dw[b].x + r1.z * dw[b].z - dvl[b].y);
-                    float dlb = grhs2 - gdinv2 * (r2.y * dw[b].y + r2.z * dw[b].z + dvl[b].x);
-                    float sa = g.lam[1] + dla, sb = g.lam[2] + dlb;
-                    float lim = gmu * g.lam[0];  // >= 0: the normal row's clamp
-                    float m2 = sa * sa + sb * sb;
-                    // |f| > mu N: project onto the cone (lim * rsq(m2) <= 1 there)
-                    float s = cone_scale(m2, lim);
-                    sa *= s;
-                    sb *= s;
-                    dla = sa - g.lam[1];
-                    dlb = sb - g.lam[2];
-                    g.lam[1] = sa;
-                    g.lam[2] = sb;
-                    if constexpr (ANISO) {
-                        // I^-1 (r1 dla + r2 dlb)
-                        dw[b] = dw[b] + od[b].inv_inertia(mk(r1.x * dla, r2.y * dlb, fmaf(r1.z, dla, r2.z * dlb)));
+                    // The two friction rows (directions (0,-1,0) and (1,0,0), so
+                    // r x dir = (r.z, 0, -r.x) and (0, r.z, -r.y)) side by side
+                    // as f32x2 (v_pk_mul/fma/add_f32): the operations the scalar
+                    // rows compiled to, fused where they were fused, so the same
+                    // bits; x = row a, y = row b.
+                    float dla, dlb;
+                    if constexpr (NOBJ == 1) {
+#pragma clang fp contract(off)
+                        const f32x2 gz = {gr.z, gr.z};
+                        const f32x2 t = (f32x2){gr.x, gr.y} * (f32x2){dw[b].z, dw[b].z};
+                        const f32x2 u = __builtin_elementwise_fma(gz, (f32x2){dw[b].x, dw[b].y}, -t);
+                        const f32x2 w = u + (f32x2){-dvl[b].y, dvl[b].x};
+                        const f32x2 lam12 = {g.lam[1], g.lam[2]};
+                        const f32x2 s2 = lam12 + __builtin_elementwise_fma(-(f32x2){gdinv1, gdinv2}, w,
+                                                                           (f32x2){grhs1, grhs2});
+                        const float lim = gmu * g.lam[0];  // >= 0: the normal row's clamp
+                        // |f| > mu N: project onto the cone (lim * rsq(m2) <= 1 there)
+                        const float sc2 = cone_scale(fmaf(s2.y, s2.y, s2.x * s2.x), lim);
+                        const f32x2 dl2 = __builtin_elementwise_fma(s2, (f32x2){sc2, sc2}, -lam12);
+                        const f32x2 nl2 = s2 * (f32x2){sc2, sc2};
+                        g.lam[1] = nl2.x;
+                        g.lam[2] = nl2.y;
+                        dla = dl2.x;
+                        dlb = dl2.y;
+                        if constexpr (ANISO) {
+                            // I^-1 (r1 dla + r2 dlb)
+                            const f32x2 zab = gz * dl2;
+                            dw[b] = dw[b] + od[b].inv_inertia(mk(zab.x, zab.y, fmaf(-gr.x, dla, -gr.y * dlb)));
+                        } else {
+                            const f32x2 ab = dl2 * (f32x2){od[b].iI, od[b].iI};
+                            const f32x2 wxy = __builtin_elementwise_fma(gz, ab, (f32x2){dw[b].x, dw[b].y});
+                            dw[b].z = fmaf(-gr.y, ab.y, fmaf(-gr.x, ab.x, dw[b].z));
+                            dw[b].x = wxy.x;
+                            dw[b].y = wxy.y;
+                        }
+                        const f32x2 vxy = __builtin_elementwise_fma((f32x2){dlb, -dla}, (f32x2){inv_m, inv_m},
+                                                                    (f32x2){dvl[b].x, dvl[b].y});
+                        dvl[b].x = vxy.x;
+                        dvl[b].y = vxy.y;
                     } else {
-                        float aI = dla * od[b].iI, bI = dlb * od[b].iI;
+                        // Stack: the scalar rows (the pairs change its bits: its
+                        // kernel contracted these expressions differently)
+                        const V3 r1 = mk(gr.z, 0.0f, -gr.x), r2 = mk(0.0f, gr.z, -gr.y);
+                        dla = grhs1 - gdinv1 * (r1.x * dw[b].x + r1.z * dw[b].z - dvl[b].y);
+                        dlb = grhs2 - gdinv2 * (r2.y * dw[b].y + r2.z * dw[b].z + dvl[b].x);
+                        float sa = g.lam[1] + dla, sb = g.lam[2] + dlb;
+                        const float lim = gmu * g.lam[0];
+                        const float m2 = sa * sa + sb * sb;
+                        const float sc2 = cone_scale(m2, lim);
+                        sa *= sc2;
+                        sb *= sc2;
+                        dla = sa - g.lam[1];
+                        dlb = sb - g.lam[2];
+                        g.lam[1] = sa;
+                        g.lam[2] = sb;
+                        const float aI = dla * od[b].iI, bI = dlb * od[b].iI;
                         dw[b].x = fmaf(r1.x, aI, dw[b].x);
                         dw[b].y = fmaf(r2.y, bI, dw[b].y);
                         dw[b].z = fmaf(r2.z, bI, fmaf(r1.z, aI, dw[b].z));
+                        dvl[b].x = fmaf(dlb, inv_m, dvl[b].x);
+                        dvl[b].y = fmaf(-dla, inv_m, dvl[b].y);
                     }
-                    dvl[b].x = fmaf(dlb, inv_m, dvl[b].x);
-                    dvl[b].y = fmaf(-dla, inv_m, dvl[b].y);
                     res = res_max(res, res_max(row_viol(dla, gdinv1), row_viol(dlb, gdinv2)));
                 }
         }
@@ -2913,10 +2955,10 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         dw[0] = dw[0] + od[0].inv_inertia(fma3(r.rn[2], -dlb, r.rn[1] * -dla));
                     } else {
                         float aI = -dla * od[0].iI, bI = -dlb * od[0].iI;
-                        dw[0] = fma3(r.rn[2], bI, fma3(r.rn[1], aI, dw[0]));
+                        dw[0] = pk_fma3(r.rn[2], bI, pk_fma3(r.rn[1], aI, dw[0]));
                     }
                     float am = -dla * od[0].inv_m, bm = -dlb * od[0].inv_m;
-                    dvl[0] = fma3(r.dir[2], bm, fma3(r.dir[1], am, dvl[0]));
+                    dvl[0] = pk_fma3(r.dir[2], bm, pk_fma3(r.dir[1], am, dvl[0]));
                 } else if constexpr (NOBJ == 2) {
                     float im = r.o1 ? od[NB - 1].inv_m : od[0].inv_m;
                     // two objects are cubes (isotropic inverse inertia)
