@@ -1643,9 +1643,19 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         for (int k = k0 + 1; k < K; k++) p = fmaf(J[k], dvm[k], p);
         return p;
     };
+    // G = 8: a lane's two DoFs updated by one v_pk_fma_f32 (the same bits)
+    auto apply2 = [&](float m0, float m1, float dl) {
+        const f32x2 x = __builtin_elementwise_fma((f32x2){m0, m1}, (f32x2){dl, dl}, (f32x2){dvm[0], dvm[K - 1]});
+        dvm[0] = x.x;
+        dvm[K - 1] = x.y;
+    };
     auto apply = [&](auto KL, const float M[K], float dl) {
+        if constexpr (K == 2 && decltype(KL)::value == 0) {
+            apply2(M[0], M[1], dl);
+        } else {
 #pragma unroll
-        for (int k = decltype(KL)::value; k < K; k++) dvm[k] = fmaf(M[k], dl, dvm[k]);
+            for (int k = decltype(KL)::value; k < K; k++) dvm[k] = fmaf(M[k], dl, dvm[k]);
+        }
     };
     // warm start (see the one-lane solver)
 #pragma unroll
@@ -1666,8 +1676,12 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
         dl = nl - lam;
         lam = nl;
         PS_REC(dl);
+        if constexpr (K == 2) {
+            apply2(mrow[0][d], mrow[K - 1][d], sgn * dl);
+        } else {
 #pragma unroll
-        for (int k = 0; k < K; k++) dvm[k] = fmaf(mrow[k][d], sgn * dl, dvm[k]);
+            for (int k = 0; k < K; k++) dvm[k] = fmaf(mrow[k][d], sgn * dl, dvm[k]);
+        }
         res = res_max(res, joint_viol(dl, midg[d]));
     };
     auto limit_row = [&](auto DD) {
@@ -1698,21 +1712,53 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
     };
     auto cone = [&](auto KL, const float J[3][K], const float M[3][K], const float rhs[3], const float dinv[3],
                     float lam[3], float mu) {
-        float sa = group_sum<G>(prod(KL, J[1])), sb = group_sum<G>(prod(KL, J[2]));
-        float dla = rhs[1] - dinv[1] * sa, dlb = rhs[2] - dinv[2] * sb;
-        float a = lam[1] + dla, b = lam[2] + dlb;
-        float lim = mu * lam[0];  // lam[0] >= 0: the normal row's clamp
-        float sc = cone_scale(a * a + b * b, lim);
-        a *= sc;
-        b *= sc;
-        dla = a - lam[1];
-        dlb = b - lam[2];
-        lam[1] = a;
-        lam[2] = b;
+        // G = 8: the two rows side by side as f32x2 (v_pk_*) around their
+        // group sums: the scalar rows' operations, fused where they were
+        // fused, so the same bits (x = row 1, y = row 2).  G = 16 keeps the
+        // scalar rows: fewer instructions with the pairs, but 0.8 % slower at
+        // C2 (profiles/r05aa_ab.log)
+        float dla, dlb;
+        if constexpr (K == 1) {
+            const float sa = group_sum<G>(prod(KL, J[1])), sb = group_sum<G>(prod(KL, J[2]));
+            dla = rhs[1] - dinv[1] * sa;
+            dlb = rhs[2] - dinv[2] * sb;
+            float a = lam[1] + dla, b = lam[2] + dlb;
+            const float lim = mu * lam[0];  // lam[0] >= 0: the normal row's clamp
+            const float sc = cone_scale(a * a + b * b, lim);
+            a *= sc;
+            b *= sc;
+            dla = a - lam[1];
+            dlb = b - lam[2];
+            lam[1] = a;
+            lam[2] = b;
+        } else {
+#pragma clang fp contract(off)
+            constexpr int k0 = decltype(KL)::value;
+            f32x2 p = (f32x2){J[1][k0], J[2][k0]} * (f32x2){dvm[k0], dvm[k0]};
+#pragma unroll
+            for (int k = k0 + 1; k < K; k++)
+                p = __builtin_elementwise_fma((f32x2){J[1][k], J[2][k]}, (f32x2){dvm[k], dvm[k]}, p);
+            const f32x2 s2 = {group_sum<G>(p.x), group_sum<G>(p.y)};
+            const f32x2 lam12 = {lam[1], lam[2]};
+            const f32x2 ab = lam12 + __builtin_elementwise_fma(-(f32x2){dinv[1], dinv[2]}, s2, (f32x2){rhs[1], rhs[2]});
+            const float lim = mu * lam[0];  // lam[0] >= 0: the normal row's clamp
+            const float sc = cone_scale(fmaf(ab.x, ab.x, ab.y * ab.y), lim);
+            const f32x2 dl2 = __builtin_elementwise_fma(ab, (f32x2){sc, sc}, -lam12);
+            const f32x2 nl2 = ab * (f32x2){sc, sc};
+            lam[1] = nl2.x;
+            lam[2] = nl2.y;
+            dla = dl2.x;
+            dlb = dl2.y;
+        }
         PS_REC(dla);
         PS_REC(dlb);
+        if constexpr (K == 2 && decltype(KL)::value == 0) {
+            apply2(M[1][0], M[1][1], dla);
+            apply2(M[2][0], M[2][1], dlb);
+        } else {
 #pragma unroll
-        for (int k = decltype(KL)::value; k < K; k++) dvm[k] = fmaf(M[2][k], dlb, fmaf(M[1][k], dla, dvm[k]));
+            for (int k = decltype(KL)::value; k < K; k++) dvm[k] = fmaf(M[2][k], dlb, fmaf(M[1][k], dla, dvm[k]));
+        }
         res = res_max(res, res_max(row_viol(dla, dinv[1]), row_viol(dlb, dinv[2])));
     };
     // the object's ground normals touch only object DoFs: they commute with
@@ -2930,17 +2976,38 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     ja -= dot(r.rn[1], ow) + dot(r.dir[1], ov);
                     jb -= dot(r.rn[2], ow) + dot(r.dir[2], ov);
                 }
-                float dla = r.rhs[1] - r.dinv[1] * ja, dlb = r.rhs[2] - r.dinv[2] * jb;
-                float sa = r.lam[1] + dla, sb = r.lam[2] + dlb;
-                float lim = r.mu * r.lam[0];  // >= 0: the normal row's clamp
-                float m2 = sa * sa + sb * sb;
-                float s = cone_scale(m2, lim);
-                sa *= s;
-                sb *= s;
-                dla = sa - r.lam[1];
-                dlb = sb - r.lam[2];
-                r.lam[1] = sa;
-                r.lam[2] = sb;
+                float dla, dlb;
+                if constexpr (NOBJ != 2) {
+                    // from the two rows' velocities on, the rows side by side as
+                    // f32x2 (v_pk_*) with the scalar rows' operations and
+                    // fusions (the same bits); the dot products stay scalar
+                    // (pairing J[1] with J[2] there costs more moves than it saves)
+#pragma clang fp contract(off)
+                    const f32x2 lam12 = {r.lam[1], r.lam[2]};
+                    const f32x2 s2 = lam12 + __builtin_elementwise_fma(-(f32x2){r.dinv[1], r.dinv[2]}, (f32x2){ja, jb},
+                                                                       (f32x2){r.rhs[1], r.rhs[2]});
+                    const float lim = r.mu * r.lam[0];  // >= 0: the normal row's clamp
+                    const float sc2 = cone_scale(fmaf(s2.x, s2.x, s2.y * s2.y), lim);
+                    const f32x2 dl2 = __builtin_elementwise_fma(s2, (f32x2){sc2, sc2}, -lam12);
+                    const f32x2 nl2 = s2 * (f32x2){sc2, sc2};
+                    r.lam[1] = nl2.x;
+                    r.lam[2] = nl2.y;
+                    dla = dl2.x;
+                    dlb = dl2.y;
+                } else {
+                    dla = r.rhs[1] - r.dinv[1] * ja;
+                    dlb = r.rhs[2] - r.dinv[2] * jb;
+                    float sa = r.lam[1] + dla, sb = r.lam[2] + dlb;
+                    const float lim = r.mu * r.lam[0];  // >= 0: the normal row's clamp
+                    const float m2 = sa * sa + sb * sb;
+                    const float s = cone_scale(m2, lim);
+                    sa *= s;
+                    sb *= s;
+                    dla = sa - r.lam[1];
+                    dlb = sb - r.lam[2];
+                    r.lam[1] = sa;
+                    r.lam[2] = sb;
+                }
                 if constexpr (NOBJ == 2) {
                     float g[9];
 #pragma unroll
