@@ -409,7 +409,9 @@ def main():
         out["roofline"]["fp32_executed"] = {
             "achieved_tflops": round(rate, 3), "peak_tflops": VALU_PEAK_TFLOPS, "frac": round(rate / VALU_PEAK_TFLOPS, 4),
             "flops_per_launch": executed,
-            "source": "profiles/pmc_traffic.json (SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32 x 64 lanes, FMA = 2)"}
+            "source": "profiles/pmc_traffic.json (SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32 x 64 lanes, FMA = 2)",
+            "note": "a lower bound: the packed v_pk_{fma,mul,add}_f32 of the solver (DESIGN.md 12.12) are not "
+                    "in these counters (they fell by about two per packed instruction when the rows were packed)"}
     if rank == 0:
         ep = episode_stats.double().cpu()
         done = ep[2] > 0
