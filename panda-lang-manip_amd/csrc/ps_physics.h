@@ -2561,14 +2561,28 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         for (int b_ = 0; b_ < NB; b_++) asm volatile("" : "+s"(gate_ground[b_]));         \
     } while (0)
     if constexpr (G == 1) {
+    // dv += M^-1 e_d f: rows a >= d of column d (its lower part, which no
+    // other column pairs) as v_pk_fma_f32 over the aligned dv pairs (2k,
+    // 2k + 1), the rest as v_fma_f32 -- the same fused products
+    auto mcol_apply = [&](int d, float f) {
+        const int a0 = (d + 1) & ~1;  // first even row >= d
+#pragma unroll
+        for (int a = 0; a < 9; a++)
+            if (a < a0 || a == 8) dv[a] = fmaf(Mi[sidx(a, d)], f, dv[a]);
+#pragma unroll
+        for (int a = a0; a < 8; a += 2) {
+            const f32x2 x = __builtin_elementwise_fma((f32x2){Mi[sidx(a, d)], Mi[sidx(a + 1, d)]}, (f32x2){f, f},
+                                                      (f32x2){dv[a], dv[a + 1]});
+            dv[a] = x.x;
+            dv[a + 1] = x.y;
+        }
+    };
     auto joint_row = [&](int d, float sgn, float rhs, float &lam, float lo, float hi) {
         float dl = rhs - dinvj[d] * (sgn * dv[d]);
         float nl = clamp_impulse(lam + dl, lo, hi);
         dl = nl - lam;
         lam = nl;
-        float f = sgn * dl;
-#pragma unroll
-        for (int a = 0; a < 9; a++) dv[a] += Mi[sidx(a, d)] * f;
+        mcol_apply(d, sgn * dl);
         res = res_max(res, joint_viol(dl, Mi[sidx(d, d)]));
     };
     auto limit_row = [&](int d) {
@@ -2621,13 +2635,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     // registers per contact and sweep); the normal rows read their M^-1 J^T
     // from the global stash (GRIP_MJ_SLOTS)
     auto mi_apply = [&](const float g[9]) {
+        // column by column: each dv[a] still takes b = 0..8 in order (the
+        // same bits as a row-by-row product), with the columns' lower parts
+        // packed (mcol_apply)
 #pragma unroll
-        for (int a = 0; a < 9; a++) {
-            float s = dv[a];
-#pragma unroll
-            for (int b = 0; b < 9; b++) s = fmaf(Mi[sidx(a, b)], g[b], s);
-            dv[a] = s;
-        }
+        for (int b = 0; b < 9; b++) mcol_apply(b, g[b]);
     };
     (void)mi_apply;
 
