@@ -2621,10 +2621,10 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         return dot(rn0, dw[0]) + dot(d, dvl[0]) - dot(rn1, dw[NB - 1]) - dot(d, dvl[NB - 1]);
     };
     auto pair_apply = [&](V3 rn0, V3 rn1, V3 d, float sdl) {
-        dw[0] = fma3(rn0, sdl * od[0].iI, dw[0]);
-        dvl[0] = fma3(d, sdl * od[0].inv_m, dvl[0]);
-        dw[NB - 1] = fma3(rn1, -sdl * od[NB - 1].iI, dw[NB - 1]);
-        dvl[NB - 1] = fma3(d, -sdl * od[NB - 1].inv_m, dvl[NB - 1]);
+        dw[0] = pk_fma3(rn0, sdl * od[0].iI, dw[0]);
+        dvl[0] = pk_fma3(d, sdl * od[0].inv_m, dvl[0]);
+        dw[NB - 1] = pk_fma3(rn1, -sdl * od[NB - 1].iI, dw[NB - 1]);
+        dvl[NB - 1] = pk_fma3(d, -sdl * od[NB - 1].inv_m, dvl[NB - 1]);
     };
     (void)pair_rel;
     (void)pair_apply;
@@ -2818,8 +2818,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 dl = nl - r.lam[0];
                 r.lam[0] = nl;
                 if constexpr (NOBJ == 2) {
-#pragma unroll
-                    for (int a = 0; a < 9; a++) dv[a] = fmaf(gmj[c][a], dl, dv[a]);
+                    pk_apply(dv, gmj[c], dl);
                 } else {
                     pk_apply(dv, mj, dl);
                 }
