@@ -481,6 +481,10 @@ PS_D V3 local_inertia(const Scene &sc, float m) {
 
 // per-substep body quantities: the world inverse inertia is a scalar for the
 // isotropic cubes and a symmetric 3x3 for the cylinder
+// two fp32 lanes of a v_pk_*_f32 instruction (the solver packs pairs of
+// independent scalar operations into them)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 template <int SHAPE>
 struct BodyDyn {
     M3 R;
@@ -752,27 +756,41 @@ struct MJStore {
     }
 };
 
-// v += m s for 9-vectors as four v_pk_fma_f32 and one v_fma_f32: the same
-// fused products, element for element, as nine v_fma_f32 (the gripper rows'
-// M^-1 J^T come from LDS as ds_read2 pairs, already in register pairs)
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-PS_D void pk_apply(float v[9], const float m[9], float s) {
-#ifdef PS_EXPERIMENT_NO_PK_APPLY
-#pragma unroll
-    for (int a = 0; a < 9; a++) v[a] = fmaf(m[a], s, v[a]);
-    return;
-#endif
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        f32x2 x = {v[2 * k], v[2 * k + 1]};
-        const f32x2 mm = {m[2 * k], m[2 * k + 1]};
-        const f32x2 ss = {s, s};
-        x = __builtin_elementwise_fma(mm, ss, x);
-        v[2 * k] = x.x;
-        v[2 * k + 1] = x.y;
+// The one-lane solver's robot velocity change, DoFs (2k, 2k + 1) as f32x2
+// values and DoF 8 alone: the pairs stay vectors through the solver loop's
+// phis, so a DoF's broadcast into a packed operand selects its half of the
+// register pair (op_sel) instead of copying it out first.
+struct VelChange {
+    f32x2 p[4];
+    float z;
+    PS_D float g(int a) const { return a == 8 ? z : p[a >> 1][a & 1]; }
+    PS_D void s(int a, float v) {
+        if (a == 8) z = v;
+        else p[a >> 1][a & 1] = v;
     }
-    v[8] = fmaf(m[8], s, v[8]);
-}
+    // (dv_a, dv_a): the broadcast of one DoF
+    PS_D f32x2 bc(int a) const {
+        if (a == 8) return (f32x2){z, z};
+        return (a & 1) ? __builtin_shufflevector(p[a >> 1], p[a >> 1], 1, 1)
+                       : __builtin_shufflevector(p[a >> 1], p[a >> 1], 0, 0);
+    }
+    // dv += m s as four v_pk_fma_f32 and one v_fma_f32: the same fused
+    // products, element for element, as nine v_fma_f32 (the gripper rows'
+    // M^-1 J^T come from LDS as ds_read2 pairs, already in register pairs)
+    PS_D void apply(const float m[9], float sc) {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            p[k] = __builtin_elementwise_fma((f32x2){m[2 * k], m[2 * k + 1]}, (f32x2){sc, sc}, p[k]);
+        z = fmaf(m[8], sc, z);
+    }
+    // J . dv as the scalar chain fma(J_a, dv_a, s) from s = 0 (jrow_dot)
+    PS_D float dot(const float J[9]) const {
+        float acc = 0.0f;
+#pragma unroll
+        for (int a = 0; a < 9; a++) acc = fmaf(J[a], g(a), acc);
+        return acc;
+    }
+};
 
 // fma3 with x and y as one v_pk_fma_f32 (the same bits)
 PS_D V3 pk_fma3(V3 a, float s, V3 c) {
@@ -2561,6 +2579,10 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         for (int b_ = 0; b_ < NB; b_++) asm volatile("" : "+s"(gate_ground[b_]));         \
     } while (0)
     if constexpr (G == 1) {
+    VelChange dvv;
+#pragma unroll
+    for (int k = 0; k < 4; k++) dvv.p[k] = (f32x2){0.0f, 0.0f};
+    dvv.z = 0.0f;
     // dv += M^-1 e_d f: rows a >= d of column d (its lower part, which no
     // other column pairs) as v_pk_fma_f32 over the aligned dv pairs (2k,
     // 2k + 1), the rest as v_fma_f32 -- the same fused products
@@ -2568,17 +2590,14 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         const int a0 = (d + 1) & ~1;  // first even row >= d
 #pragma unroll
         for (int a = 0; a < 9; a++)
-            if (a < a0 || a == 8) dv[a] = fmaf(Mi[sidx(a, d)], f, dv[a]);
+            if (a < a0 || a == 8) dvv.s(a, fmaf(Mi[sidx(a, d)], f, dvv.g(a)));
 #pragma unroll
-        for (int a = a0; a < 8; a += 2) {
-            const f32x2 x = __builtin_elementwise_fma((f32x2){Mi[sidx(a, d)], Mi[sidx(a + 1, d)]}, (f32x2){f, f},
-                                                      (f32x2){dv[a], dv[a + 1]});
-            dv[a] = x.x;
-            dv[a + 1] = x.y;
-        }
+        for (int a = a0; a < 8; a += 2)
+            dvv.p[a >> 1] = __builtin_elementwise_fma((f32x2){Mi[sidx(a, d)], Mi[sidx(a + 1, d)]}, (f32x2){f, f},
+                                                      dvv.p[a >> 1]);
     };
     auto joint_row = [&](int d, float sgn, float rhs, float &lam, float lo, float hi) {
-        float dl = rhs - dinvj[d] * (sgn * dv[d]);
+        float dl = rhs - dinvj[d] * (sgn * dvv.g(d));
         float nl = clamp_impulse(lam + dl, lo, hi);
         dl = nl - lam;
         lam = nl;
@@ -2687,8 +2706,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     for (int a = 0; a < 9; a++) g[a] = Jl[a] * l0;
                     mi_apply(g);
                 } else {
+                    float w[9];
 #pragma unroll
-                    for (int a = 0; a < 9; a++) dv[a] = fmaf(W.at(c, 0, a), l0, dv[a]);
+                    for (int a = 0; a < 9; a++) w[a] = W.at(c, 0, a);
+#pragma unroll
+                    for (int a = 0; a < 9; a++) dvv.s(a, fmaf(w[a], l0, dvv.g(a)));
                 }
                 if constexpr (NOBJ > 0) {
                     float im = NOBJ == 2 && r.o1 ? od[NB - 1].inv_m : od[0].inv_m;
@@ -2811,16 +2833,16 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     for (int a = 0; a < 9; a++) mj[a] = L.at(c, 0, a);
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                float jv = jrow_dot(Jl, dv);
+                float jv = dvv.dot(Jl);
                 if (NOBJ > 0) jv -= dot(r.rn[0], obj_dw(r.o1)) + dot(r.dir[0], obj_dv(r.o1));
                 float dl = r.rhs[0] - r.dinv[0] * jv;
                 float nl = clamp_impulse(r.lam[0] + dl, 0.0f, (float)PM_CONTACT_UPPER);
                 dl = nl - r.lam[0];
                 r.lam[0] = nl;
                 if constexpr (NOBJ == 2) {
-                    pk_apply(dv, gmj[c], dl);
+                    dvv.apply(gmj[c], dl);
                 } else {
-                    pk_apply(dv, mj, dl);
+                    dvv.apply(mj, dl);
                 }
                 if constexpr (NOBJ == 1) {
                     // one object: fma straight into its velocity change
@@ -2981,7 +3003,20 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     }
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                float ja = jrow_dot(J1, dv), jb = jrow_dot(J2, dv);
+                float ja, jb;
+                if constexpr (NOBJ != 2) {
+                    // the two rows' dot products side by side: (J1_a, J2_a) x
+                    // (dv_a, dv_a), each lane the scalar chain's FMAs
+#pragma clang fp contract(off)
+                    f32x2 j2 = {0.0f, 0.0f};
+#pragma unroll
+                    for (int a = 0; a < 9; a++) j2 = __builtin_elementwise_fma((f32x2){J1[a], J2[a]}, dvv.bc(a), j2);
+                    ja = j2.x;
+                    jb = j2.y;
+                } else {
+                    ja = dvv.dot(J1);
+                    jb = dvv.dot(J2);
+                }
                 if (NOBJ > 0) {
                     V3 ow = obj_dw(r.o1), ov = obj_dv(r.o1);
                     ja -= dot(r.rn[1], ow) + dot(r.dir[1], ov);
@@ -3025,8 +3060,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     for (int a = 0; a < 9; a++) g[a] = fmaf(J2[a], dlb, J1[a] * dla);
                     mi_apply(g);
                 } else {
-                    pk_apply(dv, mj1, dla);
-                    pk_apply(dv, mj2, dlb);
+                    dvv.apply(mj1, dla);
+                    dvv.apply(mj2, dlb);
                 }
                 if constexpr (NOBJ == 1) {
                     if constexpr (ANISO) {
@@ -3125,6 +3160,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         contacts();
         if (res <= 0.0f) break;
     }
+#pragma unroll
+    for (int a = 0; a < 9; a++) dv[a] = dvv.g(a);
     } else {
         group_pgs<NOBJ, SHAPE, STD_MOTORS, G>(mt, Mi, lds, gate_lim, lim_up, lim_on, gate_ground[0], gate_robot,
                                               dinvj, lim_rhs, lim_lam, mot_rhs, mot_lam, gc[0], rc, od[0], gmu,

@@ -34,9 +34,6 @@ VARIANTS = {
     # the group sums with FMA contraction left on (the round-3 miscompute?
     # DESIGN.md §12.6)
     "group_contract": ["-DPS_EXPERIMENT_GROUP_SUM_CONTRACT"],
-    # the gripper rows' velocity updates as nine v_fma_f32 instead of four
-    # v_pk_fma_f32 + one (pk_apply; the same bits)
-    "no_pk": ["-DPS_EXPERIMENT_NO_PK_APPLY"],
 
 }
 
