@@ -3026,8 +3026,9 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 if constexpr (NOBJ != 2) {
                     // from the two rows' velocities on, the rows side by side as
                     // f32x2 (v_pk_*) with the scalar rows' operations and
-                    // fusions (the same bits); the dot products stay scalar
-                    // (pairing J[1] with J[2] there costs more moves than it saves)
+                    // fusions (the same bits); the object's dot products above
+                    // stay scalar (pairing rn[1] with rn[2] would fight
+                    // pk_fma3's (x, y) pairs of the same registers)
 #pragma clang fp contract(off)
                     const f32x2 lam12 = {r.lam[1], r.lam[2]};
                     const f32x2 s2 = lam12 + __builtin_elementwise_fma(-(f32x2){r.dinv[1], r.dinv[2]}, (f32x2){ja, jb},
