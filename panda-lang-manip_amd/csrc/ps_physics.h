@@ -485,6 +485,25 @@ PS_D V3 local_inertia(const Scene &sc, float m) {
 // independent scalar operations into them)
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
+// mul(S3, V3) with rows x and y as v_pk_* pairs, for the solver loop's
+// velocity updates: each lane computes what the scalar row compiles to there,
+// fma(I_xz, v_z, fma(I_xx, v_x, I_xy v_y)) for row x, so the same bits
+PS_D V3 mul_pk(const S3 &I, V3 v) {
+#pragma clang fp contract(off)
+    f32x2 xy = (f32x2){I.xy, I.yy} * (f32x2){v.y, v.y};
+    xy = __builtin_elementwise_fma((f32x2){I.xx, I.xy}, (f32x2){v.x, v.x}, xy);
+    xy = __builtin_elementwise_fma((f32x2){I.xz, I.yz}, (f32x2){v.z, v.z}, xy);
+    return mk(xy.x, xy.y, fmaf(I.zz, v.z, fmaf(I.xz, v.x, I.yz * v.y)));
+}
+// the same product inside a `fp contract(off)` block: three products and two
+// sums per row
+PS_D V3 mul_pk_unfused(const S3 &I, V3 v) {
+#pragma clang fp contract(off)
+    const f32x2 xy = ((f32x2){I.xx, I.xy} * (f32x2){v.x, v.x} + (f32x2){I.xy, I.yy} * (f32x2){v.y, v.y}) +
+                     (f32x2){I.xz, I.yz} * (f32x2){v.z, v.z};
+    return mk(xy.x, xy.y, (I.xz * v.x + I.yz * v.y) + I.zz * v.z);
+}
+
 template <int SHAPE>
 struct BodyDyn {
     M3 R;
@@ -492,6 +511,15 @@ struct BodyDyn {
     S3 Ii;
     PS_D V3 inv_inertia(V3 v) const {
         if constexpr (SHAPE == SHAPE_CYL) return mul(Ii, v);
+        else return v * iI;
+    }
+    // the solver loop's: rows x and y packed (mul_pk, mul_pk_unfused)
+    PS_D V3 inv_inertia_pk(V3 v) const {
+        if constexpr (SHAPE == SHAPE_CYL) return mul_pk(Ii, v);
+        else return v * iI;
+    }
+    PS_D V3 inv_inertia_pk_unfused(V3 v) const {
+        if constexpr (SHAPE == SHAPE_CYL) return mul_pk_unfused(Ii, v);
         else return v * iI;
     }
 };
@@ -2846,7 +2874,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 }
                 if constexpr (NOBJ == 1) {
                     // one object: fma straight into its velocity change
-                    dw[0] = ANISO ? dw[0] + od[0].inv_inertia(r.rn[0] * -dl) : pk_fma3(r.rn[0], -dl * od[0].iI, dw[0]);
+                    dw[0] = ANISO ? dw[0] + od[0].inv_inertia_pk(r.rn[0] * -dl) : pk_fma3(r.rn[0], -dl * od[0].iI, dw[0]);
                     dvl[0] = pk_fma3(r.dir[0], -dl * od[0].inv_m, dvl[0]);
                 } else if constexpr (NOBJ == 2) {
                     float im = r.o1 ? od[NB - 1].inv_m : od[0].inv_m;
@@ -2917,7 +2945,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         if constexpr (ANISO) {
                             // I^-1 (r1 dla + r2 dlb)
                             const f32x2 zab = gz * dl2;
-                            dw[b] = dw[b] + od[b].inv_inertia(mk(zab.x, zab.y, fmaf(-gr.x, dla, -gr.y * dlb)));
+                            dw[b] = dw[b] + od[b].inv_inertia_pk_unfused(mk(zab.x, zab.y, fmaf(-gr.x, dla, -gr.y * dlb)));
                         } else {
                             const f32x2 ab = dl2 * (f32x2){od[b].iI, od[b].iI};
                             const f32x2 wxy = __builtin_elementwise_fma(gz, ab, (f32x2){dw[b].x, dw[b].y});
@@ -3066,7 +3094,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 }
                 if constexpr (NOBJ == 1) {
                     if constexpr (ANISO) {
-                        dw[0] = dw[0] + od[0].inv_inertia(fma3(r.rn[2], -dlb, r.rn[1] * -dla));
+                        dw[0] = dw[0] + od[0].inv_inertia_pk(fma3(r.rn[2], -dlb, r.rn[1] * -dla));
                     } else {
                         float aI = -dla * od[0].iI, bI = -dlb * od[0].iI;
                         dw[0] = pk_fma3(r.rn[2], bI, pk_fma3(r.rn[1], aI, dw[0]));
@@ -3104,7 +3132,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                 dl = nl - g.lam[0];
                 g.lam[0] = nl;
                 if constexpr (ANISO) {
-                    dw[0] = dw[0] + od[0].inv_inertia(mk(rn.x * dl, rn.y * dl, 0.0f));
+                    dw[0] = dw[0] + od[0].inv_inertia_pk(mk(rn.x * dl, rn.y * dl, 0.0f));
                 } else {
                     const float dI = dl * od[0].iI;
                     dw[0].x = fmaf(rn.x, dI, dw[0].x);
