@@ -2924,7 +2924,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     // rows compiled to, fused where they were fused, so the same
                     // bits; x = row a, y = row b.
                     float dla, dlb;
-                    if constexpr (NOBJ == 1) {
+                    {
 #pragma clang fp contract(off)
                         const f32x2 gz = {gr.z, gr.z};
                         const f32x2 t = (f32x2){gr.x, gr.y} * (f32x2){dw[b].z, dw[b].z};
@@ -2934,8 +2934,11 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                         const f32x2 s2 = lam12 + __builtin_elementwise_fma(-(f32x2){gdinv1, gdinv2}, w,
                                                                            (f32x2){grhs1, grhs2});
                         const float lim = gmu * g.lam[0];  // >= 0: the normal row's clamp
+                        // |f|^2 as each kernel's scalar rows contracted it (the
+                        // one-object kernels fused row b's square, Stack's row a's);
                         // |f| > mu N: project onto the cone (lim * rsq(m2) <= 1 there)
-                        const float sc2 = cone_scale(fmaf(s2.y, s2.y, s2.x * s2.x), lim);
+                        const float m2 = NOBJ == 2 ? fmaf(s2.x, s2.x, s2.y * s2.y) : fmaf(s2.y, s2.y, s2.x * s2.x);
+                        const float sc2 = cone_scale(m2, lim);
                         const f32x2 dl2 = __builtin_elementwise_fma(s2, (f32x2){sc2, sc2}, -lam12);
                         const f32x2 nl2 = s2 * (f32x2){sc2, sc2};
                         g.lam[1] = nl2.x;
@@ -2957,28 +2960,6 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                                                                     (f32x2){dvl[b].x, dvl[b].y});
                         dvl[b].x = vxy.x;
                         dvl[b].y = vxy.y;
-                    } else {
-                        // Stack: the scalar rows (the pairs change its bits: its
-                        // kernel contracted these expressions differently)
-                        const V3 r1 = mk(gr.z, 0.0f, -gr.x), r2 = mk(0.0f, gr.z, -gr.y);
-                        dla = grhs1 - gdinv1 * (r1.x * dw[b].x + r1.z * dw[b].z - dvl[b].y);
-                        dlb = grhs2 - gdinv2 * (r2.y * dw[b].y + r2.z * dw[b].z + dvl[b].x);
-                        float sa = g.lam[1] + dla, sb = g.lam[2] + dlb;
-                        const float lim = gmu * g.lam[0];
-                        const float m2 = sa * sa + sb * sb;
-                        const float sc2 = cone_scale(m2, lim);
-                        sa *= sc2;
-                        sb *= sc2;
-                        dla = sa - g.lam[1];
-                        dlb = sb - g.lam[2];
-                        g.lam[1] = sa;
-                        g.lam[2] = sb;
-                        const float aI = dla * od[b].iI, bI = dlb * od[b].iI;
-                        dw[b].x = fmaf(r1.x, aI, dw[b].x);
-                        dw[b].y = fmaf(r2.y, bI, dw[b].y);
-                        dw[b].z = fmaf(r2.z, bI, fmaf(r1.z, aI, dw[b].z));
-                        dvl[b].x = fmaf(dlb, inv_m, dvl[b].x);
-                        dvl[b].y = fmaf(-dla, inv_m, dvl[b].y);
                     }
                     res = res_max(res, res_max(row_viol(dla, gdinv1), row_viol(dlb, gdinv2)));
                 }
