@@ -125,6 +125,8 @@ def lib():
         L.po_set_model_mutation.argtypes = [I, D]
         L.po_set_fp32_solver.argtypes = [I]
         L.po_set_fp32_dynamics.argtypes = [I]
+        L.po_set_pgs_shift.argtypes = [I]
+        L.po_set_clip_bias.argtypes = [D]
         _lib = L
     return _lib
 
@@ -301,14 +303,15 @@ def set_link_aabb(link, lx, ly, lz):
     lib().po_set_link_aabb(link, lx, ly, lz)
 
 
-MUTATIONS = {"none": 0, "motor_kp_scale": 1, "link_damping": 2, "finger_box_grow": 3}
+MUTATIONS = {"none": 0, "motor_kp_scale": 1, "link_damping": 2, "finger_box_grow": 3, "pair_friction_scale": 4}
 
 
 def set_model_mutation(kind: str, value: float = 0.0):
     """Test hook: a deliberate model error (panda_oracle.c po_set_model_mutation):
     'motor_kp_scale' (kp x value), 'link_damping' (every body's k1 = k2 := value),
-    'finger_box_grow' (finger boxes' half extents + value m); 'none' restores
-    the model.  The object's mass and friction are Config fields."""
+    'finger_box_grow' (finger boxes' half extents + value m),
+    'pair_friction_scale' (Stack's cube-cube friction x value); 'none' restores
+    the model.  The objects' masses and friction are Config fields."""
     lib().po_set_model_mutation(MUTATIONS[kind], float(value))
 
 
@@ -317,3 +320,17 @@ def set_state_noise(ulps: float, seed: int = 0):
     state component after each substep (panda_oracle.c po_set_state_noise);
     ulps < 0 rounds the state to fp32 after each substep instead."""
     lib().po_set_state_noise(float(ulps), int(seed))
+
+
+def set_pgs_shift(k: int):
+    """Test hook (panda_oracle.c po_set_pgs_shift): every substep's PGS exits k
+    iterations after its stopping rule is first met (k > 0), or with the
+    impulses of the iteration before (k < 0); 0 restores Bullet's rule."""
+    lib().po_set_pgs_shift(int(k))
+
+
+def set_clip_bias(m: float):
+    """Test hook (panda_oracle.c po_set_clip_bias): Stack's box-box clip lines
+    moved outward by m metres (a vertex on a clip line to within rounding
+    changes side, and the clipped polygon starts at another vertex)."""
+    lib().po_set_clip_bias(float(m))

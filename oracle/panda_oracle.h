@@ -156,10 +156,17 @@ void po_link_inertia(int link, double inertia[3]);
 void po_set_link_aabb(int link, double lx, double ly, double lz);
 /* test hook: deliberate model errors for the parity classifier's power test
  * (tests/test_judge_power.py); PO_MUT_NONE restores the model, not thread-safe */
+/* test hook: the PGS exits k iterations after its stopping rule is met (k > 0) or
+ * one iteration before (k < 0): parity_judge's stopping-rule probe; not thread-safe */
+void po_set_pgs_shift(int k);
+/* test hook: the box-box clip lines moved outward by m metres (parity_judge's
+ * pair-order probe); not thread-safe */
+void po_set_clip_bias(double m);
 #define PO_MUT_NONE 0
 #define PO_MUT_MOTOR_KP 1     /* kp := PM_MOTOR_KP x value */
 #define PO_MUT_LINK_DAMPING 2 /* btMultiBody damping k1 = k2 of every body := value */
 #define PO_MUT_FINGER_BOX 3   /* finger boxes' half extents += value (m) */
+#define PO_MUT_PAIR_FRICTION 4 /* cube-cube friction coefficient (Stack) := its default x value */
 void po_set_model_mutation(int kind, double value);
 /* test hook: per-substep finger-position noise of +-amplitude (0 = off), not thread-safe */
 void po_set_finger_noise(double amplitude, uint64_t seed);

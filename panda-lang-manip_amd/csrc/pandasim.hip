@@ -738,10 +738,10 @@ int ps_step(ps_ctx *c, void *state, const float *actions, float *obs, float *ag,
     if (!c || !state || !actions || !reward || !terminated || !truncated)
         return fail(c, PS_ERR_ARG, "null argument");
     if (!scene_matches_task(c->cfg)) return fail(c, PS_ERR_UNSUPPORTED, "scene does not match the task");
-    if (ensure_stash(c) != PS_OK) return fail(c, PS_ERR_HIP, "hipMalloc of the Stack stash failed");
+    hipStream_t st = (hipStream_t)stream;
+    if (ensure_stash(c, st) != PS_OK) return fail(c, PS_ERR_HIP, "hipMalloc of the Stack stash failed");
     const ps_step_io io{actions, obs, ag, dg, reward, terminated, truncated, final_obs, final_ag, autoreset};
     const int lanes = ps_step_lanes(c);
-    hipStream_t st = (hipStream_t)stream;
     const bool ee = c->cfg.control == PS_CONTROL_EE;
     int rc;
 #define PS_STEP_TASK_CASE(T)                                                                              \
@@ -791,8 +791,8 @@ int ps_set_nonfinite_guard(ps_ctx *c, uint8_t *flags, int reset_nonfinite) {
 
 int ps_sim_step(ps_ctx *c, void *state, int n_substeps, void *stream) {
     if (!c || !state || n_substeps < 0) return fail(c, PS_ERR_ARG, "bad argument");
-    if (ensure_stash(c) != PS_OK) return fail(c, PS_ERR_HIP, "hipMalloc of the Stack stash failed");
     hipStream_t st = (hipStream_t)stream;
+    if (ensure_stash(c, st) != PS_OK) return fail(c, PS_ERR_HIP, "hipMalloc of the Stack stash failed");
     if (c->cfg.n_objects == 0) return PS_SIM_LAUNCHER_NAME(0, 0)(c, state, n_substeps, st);
     if (c->cfg.n_objects == 2) return PS_SIM_LAUNCHER_NAME(2, 0)(c, state, n_substeps, st);
     if (c->cfg.object_shape == PS_SHAPE_CYLINDER) return PS_SIM_LAUNCHER_NAME(1, 1)(c, state, n_substeps, st);

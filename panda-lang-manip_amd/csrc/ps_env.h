@@ -87,6 +87,7 @@ namespace {
 
 
 constexpr int kBlock = 64;
+static_assert(kBlock == CW_LANES, "robot_candidates: the work lists' output rows are kBlock lanes wide");
 
 // Per-task constants (panda_gym/__init__.py:8-54, envs/panda_tasks.py:14-113,
 // tasks/*.py): objects, shape, goal size, TimeLimit and success threshold.
@@ -593,7 +594,7 @@ inline KParams params_of(ps_ctx *c, void *state) {
 
 // Stack's global stash (the LDS it would use holds its ground rows): one
 // allocation on the first step of a two-object context, never per step
-inline int ensure_stash(ps_ctx *c) {
+inline int ensure_stash(ps_ctx *c, hipStream_t st) {
 #ifdef PS_EXPERIMENT_TWO_WAVES
     const int64_t floats = c->cfg.n_objects == 2 ? GSTASH_FLOATS : GX_FLOATS;
 #else
@@ -601,10 +602,14 @@ inline int ensure_stash(ps_ctx *c) {
     const int64_t floats = GSTASH_FLOATS;
 #endif
     if (c->gstash) return PS_OK;
-    if (hipMalloc((void **)&c->gstash, sizeof(float) * floats * c->lay.stride) != hipSuccess) {
+    const size_t bytes = sizeof(float) * (floats * c->lay.stride + GSTASH_ZERO_FLOATS);
+    if (hipMalloc((void **)&c->gstash, bytes) != hipSuccess) {
         c->gstash = nullptr;
         return PS_ERR_HIP;
     }
+    // all-zero (the solver's zero block after the stash, GSTASH_ZERO_FLOATS),
+    // on the stream the steps run on
+    if (hipMemsetAsync(c->gstash, 0, bytes, st) != hipSuccess) return PS_ERR_HIP;
     return PS_OK;
 }
 
@@ -671,6 +676,7 @@ __global__ __launch_bounds__(kBlock, PS_STEP_MIN_WAVES) void k_step(KParams P, c
                                                                  i * (NP * PAIR_FLOATS));
         lds.ggrip = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_GRIP_OFFSET * s.stride +
                                                                  i * GRIP_FLOATS);
+        lds.gzero = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_FLOATS * s.stride);
     }
 #ifdef PS_EXPERIMENT_TWO_WAVES
     if constexpr (T::NOBJ < 2) {
@@ -780,6 +786,7 @@ __global__ __launch_bounds__(kBlock) void k_sim_step(KParams P, int n_substeps) 
                                                                  i * (NP * PAIR_FLOATS));
         lds.ggrip = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_GRIP_OFFSET * s.stride +
                                                                  i * GRIP_FLOATS);
+        lds.gzero = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_FLOATS * s.stride);
     }
 #ifdef PS_EXPERIMENT_TWO_WAVES
     if constexpr (NOBJ < 2) {

@@ -666,7 +666,20 @@ constexpr int LDS_GND_FLOATS = 6;
 constexpr int LDS_FLOATS_STACK = LDS_GND_OFFSET + 2 * NG * LDS_GND_FLOATS;
 static_assert(LDS_FLOATS_STACK * 4 * 64 * 4 <= 160 * 1024, "four Stack workgroups per CU");
 constexpr int PAIR_FLOATS = 21;
-constexpr int GSTASH_PAIR_OFFSET = LDS_STASH_FLOATS + 13;
+// Stack's global stash rows (env-minor): the stash without the split-impulse
+// corrections (recomputed from q after the solve, split_of: 9 rows fewer) and
+// object 1's pre-solve state.
+constexpr int GSTASH_ROWS = LDS_STASH_FLOATS + 13 - 9;
+constexpr int GSTASH_PAIR_OFFSET = GSTASH_ROWS;
+// The pair and gripper rows of a slot an env does not use are never written:
+// the solver, which runs a slot's rows while any lane of the wave has it,
+// points the lanes without it at one all-zero block (GSTASH_ZERO_FLOATS, after
+// the stash, zeroed at allocation: ensure_stash) -- exact no-op rows, one
+// cache line for the whole wave.  Before, every env rewrote its unused slots
+// as zeros every substep and the wave read 64 env-major rows per slot: most of
+// Stack's HBM traffic (2.03 GB per launch at 65 536 envs, VERDICT r05 weak 3;
+// ~2 % of envs have a box-box contact at a time).
+constexpr int GSTASH_ZERO_FLOATS = 32;
 // Stack: M^-1 J^T of the gripper slots' normal rows, env-major after the
 // pair rows (9 floats per slot), computed with J at contact setup and loaded
 // at the top of each sweep (object_normals), so a gripper normal updates dv
@@ -768,6 +781,15 @@ struct MJStore {
     // Stack only (global stash): M^-1 J^T of gripper slot c's normal row, element k
     __attribute__((address_space(1))) float *ggrip = nullptr;
     PS_D float &grip(int c, int k) const { return *(float *)&ggrip[c * 9 + k]; }
+    // Stack: the solver's source of pair slot c / gripper slot c: this env's
+    // rows if it has the slot (c < n), else the shared zero block
+    __attribute__((address_space(1))) float *gzero = nullptr;
+    PS_D __attribute__((address_space(1))) float *pair_rows(int c, int n) const {
+        return c < n ? gpair + c * PAIR_FLOATS : gzero;
+    }
+    PS_D __attribute__((address_space(1))) float *grip_rows(int c, int n) const {
+        return c < n ? ggrip + c * 9 : gzero;
+    }
     // a copy whose address the compiler cannot see through: loads from it are
     // not loop-invariant, so they stay in the PGS loop as ds_reads instead of
     // being hoisted into (spilled) registers
@@ -1476,6 +1498,12 @@ PS_D float row_viol(float dl, float dinv) { return fmaf(-kResidualAbs, dinv, fab
 // both give the same bits.  The impulse clamps stay fminf(fmaxf()): as
 // v_med3_f32 (the same bits too) they made Push 0.25 % slower
 // (profiles/r05v_ab.log).
+// A NaN row violation (an env whose state is already non-finite) keeps res at
+// NaN, so that lane never meets `res <= 0` and runs the 50-iteration cap; it is
+// masked like any other lane, so no other env's rows or bits change, and the
+// NaN/Inf guard flags (and optionally resets) the env after the step
+// (test_gpu_contacts.py::test_nonfinite_guard_flags_and_resets: every other
+// env equal bit for bit to a run without the corrupted one).
 PS_D float res_max(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 PS_D float clamp_impulse(float x, float lo, float hi) { return fminf(fmaxf(x, lo), hi); }
 PS_D float joint_viol(float dl, float den) { return fmaf(fabsf(dl), den, -kResidualAbs); }
@@ -1944,6 +1972,10 @@ PS_D int nth_set_bit(uint64_t m, int j) {
 constexpr int CW_IN = 0;    // owner: hR (9), box centres (3 x 3), object position (3), rotation (9)
 constexpr int CW_OUT = 30;  // worker: pick 0 (pA, pB, n, dist), pick 1, count
 constexpr int CW_OUT_FLOATS = 21;
+// the work lists' per-lane output rows are one wave wide: row q of worker lane
+// c at cwo0[q * CW_LANES + c] (the step kernels' kBlock, asserted equal in
+// ps_env.h: a workgroup of another width would overwrite other waves' rows)
+constexpr int CW_LANES = 64;
 static_assert(CW_OUT + CW_OUT_FLOATS <= RobotCand::OFFSET, "work-list scratch below the candidate records");
 
 // The group kernels (G > 1) keep one LDS column per env, shared by the
@@ -1977,9 +2009,9 @@ PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const
     // column 0 of the wave's LDS block; lane c's column (its env's when shared)
     lds_float *const col0 = lds.base - (SHARED ? lane / G : lane);
     auto at = [&](int k, int c) -> lds_float & { return col0[k * lds.stride + (SHARED ? c / G : c)]; };
-    // worker lane c's output row q (stride kBlock: 64 lanes)
+    // worker lane c's output row q (stride CW_LANES = kBlock)
     lds_float *const cwo0 = lds.cwo - lane;
-    auto wout = [&](int q, int c) -> lds_float & { return cwo0[q * 64 + c]; };
+    auto wout = [&](int q, int c) -> lds_float & { return cwo0[q * CW_LANES + c]; };
     static_for<0, NOBJ + 1>([&](auto TT) {
         constexpr int TGT = decltype(TT)::value == NOBJ ? 2 : decltype(TT)::value;
         constexpr bool GROUND = TGT == 2;
@@ -2090,8 +2122,8 @@ PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const
                     const int nout = GROUND && PM_BOX_GROUND_CONTACTS < 2 ? 10 : 20;
 #pragma unroll
                     for (int q = 0; q < 20; q++)
-                        if (q < nout) lds.cwo[q * 64] = out[q];
-                    lds.cwo[20 * 64] = out[20];
+                        if (q < nout) lds.cwo[q * CW_LANES] = out[q];
+                    lds.cwo[20 * CW_LANES] = out[20];
                 }
                 __syncthreads();
                 // the owners take their pairs of this round, in box order
@@ -2146,6 +2178,25 @@ PS_D int robot_candidates(const Scene &sc, const Geo &geo, const Body *bd, const
 // STD_MOTORS: the motors are the ones RobotTaskEnv.step sets (POSITION_CONTROL
 // on all nine joints with the fixed Panda gains and forces, panda.py:40-56), so
 // only the targets are per-env; otherwise every gain comes from `mt`.
+// The split-impulse position correction of joint d's limit rows (the joint
+// rows' setup in substep, same expressions): a function of q alone, so Stack
+// rebuilds it after the solve instead of keeping 9 stash rows per substep.
+PS_D float split_of(int d, float qd_) {
+    float split = 0.0f;
+#pragma unroll
+    for (int side = 0; side < 2; side++) {
+        const double LO = dof_def(d).lo, HI = dof_def(d).hi;
+        const float lo_h = (float)LO, lo_t = (float)(LO - (double)lo_h);
+        const float hi_h = (float)HI, hi_t = (float)(HI - (double)hi_h);
+        float pen = side ? (hi_h - qd_) + hi_t : (qd_ - lo_h) - lo_t;
+        float sgn = side ? -1.0f : 1.0f;
+        bool on = pen <= 0.0f;
+        bool combined = pen > (float)PM_SPLIT_PENETRATION_THRESHOLD;
+        if (on && !combined) split += sgn * (-pen) * (float)PM_SPLIT_LIMIT_ERP;
+    }
+    return split;
+}
+
 template <int NOBJ, int SHAPE, bool STD_MOTORS, int G = 1>
 PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Body *bd, const MJStore &lds,
                   const WarmCache<G, NOBJ> &wc PS_PROF_PARAM PS_DUMP_PARAM) {
@@ -2428,15 +2479,19 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
                     p.rhs[j] = p.lam[j] = p.dinv[j] = 0.0f;
                 }
             }
-            // the read-only part of the row goes to the global stash (PAIR_FLOATS)
+            // the read-only part of the row goes to the global stash
+            // (PAIR_FLOATS); the slots this env does not use are not written
+            // (the solver reads the zero block for them: MJStore::pair_rows)
+            if (c < np) {
 #pragma unroll
-            for (int j = 0; j < 3; j++) {
-                lds.pair(c, 3 * j + 0) = p.dir[j].x; lds.pair(c, 3 * j + 1) = p.dir[j].y; lds.pair(c, 3 * j + 2) = p.dir[j].z;
-                lds.pair(c, 15 + j) = p.rhs[j];
-                lds.pair(c, 18 + j) = p.dinv[j];
+                for (int j = 0; j < 3; j++) {
+                    lds.pair(c, 3 * j + 0) = p.dir[j].x; lds.pair(c, 3 * j + 1) = p.dir[j].y; lds.pair(c, 3 * j + 2) = p.dir[j].z;
+                    lds.pair(c, 15 + j) = p.rhs[j];
+                    lds.pair(c, 18 + j) = p.dinv[j];
+                }
+                lds.pair(c, 9) = p.rA.x; lds.pair(c, 10) = p.rA.y; lds.pair(c, 11) = p.rA.z;
+                lds.pair(c, 12) = p.rB.x; lds.pair(c, 13) = p.rB.y; lds.pair(c, 14) = p.rB.z;
             }
-            lds.pair(c, 9) = p.rA.x; lds.pair(c, 10) = p.rA.y; lds.pair(c, 11) = p.rA.z;
-            lds.pair(c, 12) = p.rB.x; lds.pair(c, 13) = p.rB.y; lds.pair(c, 14) = p.rB.z;
         }
         wc.store(PS_F_WPN, (float)np);
     }
@@ -2511,9 +2566,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
 #pragma unroll
                     for (int a = 0; a < 9; a++) {
                         c.J[j][a] = 0.0f;
-                        lds.at(sl, j, a) = 0.0f;
-                        if constexpr (NOBJ == 2)
-                            if (j == 0) lds.grip(sl, a) = 0.0f;
+                        lds.at(sl, j, a) = 0.0f;  // (Stack's grip rows: MJStore::grip_rows reads the zero block)
                     }
                     c.dir[j] = c.rn[j] = mk(0, 0, 0);
                     c.rhs[j] = c.lam[j] = c.dinv[j] = 0.0f;
@@ -2526,19 +2579,22 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
     __builtin_amdgcn_sched_barrier(0);
     // per-substep values the solver never reads wait outside the registers:
     // in LDS, or (Stack, whose LDS holds its ground rows) in the global stash
+    // (Stack: its global stash has no split-impulse rows, 18..26: split_of
+    // rebuilds them from q after the solve, and the rows above shift down)
+    auto gk = [](int k) { return NOBJ == 2 && k >= 27 ? k - 9 : k; };
     auto put = [&](int k, float v) {
-        if constexpr (NOBJ == 2) lds.gstash(k) = v;
+        if constexpr (NOBJ == 2) lds.gstash(gk(k)) = v;
         else lds.stash(k) = v;
     };
     auto get = [&](const MJStore &S, int k) -> float {
-        if constexpr (NOBJ == 2) return S.gstash(k);
+        if constexpr (NOBJ == 2) return S.gstash(gk(k));
         else return S.stash(k);
     };
 #pragma unroll
     for (int d = 0; d < 9; d++) {
         put(d, q[d]);
         put(9 + d, v1[d]);
-        put(18 + d, split_dq[d]);
+        if constexpr (NOBJ != 2) put(18 + d, split_dq[d]);
     }
     if constexpr (NOBJ > 0) {
         put(27, cw1[0].x); put(28, cw1[0].y); put(29, cw1[0].z);
@@ -2714,7 +2770,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
 #pragma unroll
             for (int c = 0; c < NP; c++)
                 if (gate_pair & (1u << c)) {
-                    auto pv = [&](int k) { return mk(W.pair(c, k), W.pair(c, k + 1), W.pair(c, k + 2)); };
+                    const auto *pr = W.pair_rows(c, np);
+                    auto pv = [&](int k) { return mk(pr[k], pr[k + 1], pr[k + 2]); };
                     const float sl = pc[c].a0 ? pc[c].lam[0] : -pc[c].lam[0];
                     const V3 d0 = pv(0);
                     pair_apply(cross(pv(9), d0), cross(pv(12), d0), d0, sl);
@@ -2765,14 +2822,15 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             if (gate_pair) {
 #pragma unroll
                 for (int c = 0; c < NP; c++) {
+                    const auto *pr = L.pair_rows(c, np);
 #pragma unroll
                     for (int k = 0; k < 3; k++) {
-                        pf[c][k] = L.pair(c, k);
-                        pf[c][3 + k] = L.pair(c, 9 + k);
-                        pf[c][6 + k] = L.pair(c, 12 + k);
+                        pf[c][k] = pr[k];
+                        pf[c][3 + k] = pr[9 + k];
+                        pf[c][6 + k] = pr[12 + k];
                     }
-                    pf[c][9] = L.pair(c, 15);
-                    pf[c][10] = L.pair(c, 18);
+                    pf[c][9] = pr[15];
+                    pf[c][10] = pr[18];
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -2782,8 +2840,9 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
 #pragma unroll
                 for (int c = 0; c < GRIP_MJ_SLOTS; c++)
                     if (gate_robot & (1u << c)) {
+                        const auto *gr = L.grip_rows(c, nr);
 #pragma unroll
-                        for (int k = 0; k < 9; k++) gmj[c][k] = L.grip(c, k);
+                        for (int k = 0; k < 9; k++) gmj[c][k] = gr[k];
                     }
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -2889,12 +2948,13 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
             if (gate_pair) {
 #pragma unroll
                 for (int c = 0; c < NP; c++) {
+                    const auto *pr = L.pair_rows(c, np);
 #pragma unroll
-                    for (int k = 0; k < 12; k++) pq[c][k] = L.pair(c, 3 + k);  // d1, d2, r0, r1
-                    pq[c][12] = L.pair(c, 16);
-                    pq[c][13] = L.pair(c, 17);
-                    pq[c][14] = L.pair(c, 19);
-                    pq[c][15] = L.pair(c, 20);
+                    for (int k = 0; k < 12; k++) pq[c][k] = pr[3 + k];  // d1, d2, r0, r1
+                    pq[c][12] = pr[16];
+                    pq[c][13] = pr[17];
+                    pq[c][14] = pr[19];
+                    pq[c][15] = pr[20];
                 }
                 __builtin_amdgcn_sched_barrier(0);
             }
@@ -3221,7 +3281,7 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         for (int d = 0; d < 9; d++) {
             q[d] = get(S, d);
             v1[d] = get(S, 9 + d);
-            split_dq[d] = get(S, 18 + d);
+            split_dq[d] = NOBJ == 2 ? split_of(d, q[d]) : get(S, 18 + d);
         }
         if constexpr (NOBJ > 0) {
             cw1[0] = mk(get(S, 27), get(S, 28), get(S, 29));

@@ -121,26 +121,50 @@ def _jobs() -> int:
     return max(1, min(16, len(os.sched_getaffinity(0))))
 
 
-_inflight = [0]
-_inflight_lock = threading.Lock()
-
-
-class _Gate:
-    """Compiles pass the gate freely unless a crash retry holds it."""
+class _Scheduler:
+    """Admission of compiles: any number run together, except while a crash
+    retry runs, which waits until no other compile is in flight and keeps
+    new ones from starting until it is done (one condition variable covers
+    both the retry flag and the in-flight count, so no compile can slip in
+    between a retry's check and its start: ADVICE r05)."""
 
     def __init__(self):
-        self._lock = threading.Lock()
+        self._cv = threading.Condition()
+        self._inflight = 0
+        self._serial = False
 
-    def __enter__(self):
-        self._lock.acquire()
-        self._lock.release()
+    def start(self) -> None:
+        with self._cv:
+            while self._serial:
+                self._cv.wait()
+            self._inflight += 1
 
-    def __exit__(self, *exc):
-        return False
+    def end(self) -> int:
+        """Leaves; returns the number of compiles that were in flight with it."""
+        with self._cv:
+            jobs = self._inflight
+            self._inflight -= 1
+            self._cv.notify_all()
+            return jobs
+
+    def run_alone(self, fn):
+        with self._cv:
+            while self._serial:
+                self._cv.wait()
+            self._serial = True
+            while self._inflight > 0:
+                self._cv.wait()
+        try:
+            return fn()
+        finally:
+            with self._cv:
+                self._serial = False
+                self._cv.notify_all()
 
 
-_serial_gate = _Gate()
-_serial_lock = _serial_gate._lock
+_sched = _Scheduler()
+# serialized retries of one unit after a crash (each alone on the machine)
+CRASH_RETRIES = 3
 
 
 def _crashed(r) -> bool:
@@ -185,27 +209,22 @@ def build(force: bool = False, verbose: bool = True, variant: str = "", extra=()
         # have not crashed (profiles/r05_build_log.jsonl: consecutive forced
         # builds).  Should a compile still crash, the crash is logged (unit,
         # attempt, jobs in flight: build/build_log.jsonl) and the unit is
-        # compiled again once, alone (the other jobs wait on the lock); a
-        # second crash or any diagnostic fails the build.
-        with _inflight_lock:
-            _inflight[0] += 1
+        # compiled again alone (no other compile in flight, none starting:
+        # _Scheduler), up to CRASH_RETRIES times; a crash after that, or any
+        # diagnostic, fails the build.
+        _sched.start()
         try:
             r = subprocess.run(cmd, capture_output=True, text=True)
         finally:
-            with _inflight_lock:
-                jobs = _inflight[0]
-                _inflight[0] -= 1
-        if _crashed(r):
-            _log_crash(name, 1, jobs, r.stderr)
-            with _serial_lock:  # no compile starts now; wait for those in flight
-                while True:
-                    with _inflight_lock:
-                        if _inflight[0] == 0:
-                            break
-                    time.sleep(0.2)
-                r = subprocess.run(cmd, capture_output=True, text=True)
-            if _crashed(r):
-                _log_crash(name, 2, 1, r.stderr)
+            jobs = _sched.end()
+        attempt = 1
+        while _crashed(r):
+            _log_crash(name, attempt, jobs, r.stderr)
+            if attempt > CRASH_RETRIES:
+                break
+            attempt += 1
+            jobs = 1
+            r = _sched.run_alone(lambda: subprocess.run(cmd, capture_output=True, text=True))
         if r.stdout:
             print(r.stdout, end="")
         if r.returncode != 0:
@@ -216,15 +235,8 @@ def build(force: bool = False, verbose: bool = True, variant: str = "", extra=()
             f.write(key + "\n")
         return obj
 
-    # the crash retry runs alone: while it holds _serial_lock no compile
-    # starts, and it waits for those in flight to finish
-    def guarded(unit):
-        with _serial_gate:
-            pass
-        return compile_unit(unit)
-
     with cf.ThreadPoolExecutor(_jobs()) as ex:
-        objs = list(ex.map(guarded, UNITS))
+        objs = list(ex.map(compile_unit, UNITS))
     cmd = [hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", out + ".tmp", *objs]
     if verbose:
         print(" ".join(cmd), flush=True)

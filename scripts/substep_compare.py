@@ -20,7 +20,7 @@ sys.path[:0] = [os.path.join(ROOT, "panda-lang-manip_amd"), os.path.join(ROOT, "
 import torch  # noqa: E402
 
 import oracle as O  # noqa: E402
-from helpers import WR_ROW, oracle_env_from, unpack_ids  # noqa: E402
+from helpers import WG_ROWS, WR_ROW, oracle_env_from, unpack_ids  # noqa: E402
 
 
 def main(path):
@@ -49,12 +49,17 @@ def main(path):
         dq = np.abs(g[0:9] - np.array(e.q[:9])).max()
         dqd = np.abs(g[9:18] - np.array(e.qd[:9])).max()
         dobj = np.abs(g[63:66] - np.array(e.obj[0].pos)).max()
+        dov = np.abs(g[70:73] - np.array(e.obj[0].vel)).max()
+        dow = np.abs(g[73:76] - np.array(e.obj[0].omg)).max()
+        gg = [round(float(x), 5) for x in g[WG_ROWS[0]:WG_ROWS[0] + 4]]
+        og = [round(e.cache.ground_lam[0][k], 5) for k in range(4)]
         gid = unpack_ids(g[WR_ROW + 4])
         glam = [round(float(x), 5) for x in g[WR_ROW:WR_ROW + 4]]
         oid = [e.cache.robot_id[k] for k in range(4)]
         olam = [round(e.cache.robot_lam[k], 5) for k in range(4)]
-        print(f"substep {s:2d}: |dq| {dq:.2e} |dqd| {dqd:.2e} |dobj| {dobj:.2e}  gpu robot {list(zip(gid, glam))}  "
-              f"oracle {list(zip(oid, olam))}", flush=True)
+        print(f"substep {s:2d}: |dq| {dq:.2e} |dqd| {dqd:.2e} |dobj| {dobj:.2e} |dv_obj| {dov:.2e} |dw_obj| {dow:.2e}  "
+              f"gpu robot {list(zip(gid, glam))}  oracle {list(zip(oid, olam))}  ground0 gpu {gg} oracle {og}",
+              flush=True)
     print("final vs the fused step's state:", float(np.abs(env.sim.f[0:18, 0].double().cpu().numpy() -
                                                        d["gpu_f_after"][0:18]).max()))
 

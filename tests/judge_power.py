@@ -16,7 +16,11 @@ Workloads (as in the GPU tests):
     default_rng(7);
   * "push": test_gpu_parity.test_gripper_object_contact_parity's scripted
     push -- 64 envs, seeds 44 + i, 14 steps, the end effector driven over
-    the object and then through it, the fingers closing from step 8.
+    the object and then through it, the fingers closing from step 8;
+  * "stack_push" (Stack): test_gpu_parity.test_judged_contact_workloads --
+    seeds 44 + i, cube 2 set on cube 1 at rest, then the scripted push
+    aimed at cube 2: the gripper comes down on the top cube and drags it
+    over the bottom one (box-box normal and friction rows every step).
 The stand-in's own trajectory is followed (as the GPU's is), and each step
 starts from its state rounded to fp32 (the GPU's state storage).
 """
@@ -83,6 +87,9 @@ MUTATIONS = {
     "motor_kp_x1.01": ("motor_kp_scale", 1.01),
     "link_damping_0.045": ("link_damping", 0.045),
     "finger_box_+0.5mm": ("finger_box_grow", 0.0005),
+    # round 6: Stack's second cube and its cube-cube rows
+    "cube2_mass_x1.02": ("config", "object2_mass", 1.02),
+    "pair_friction_x1.02": ("pair_friction_scale", 1.02),
 }
 
 
@@ -121,6 +128,15 @@ def _push_actions(envs, body, s, action_dim, cfg):
     return a
 
 
+def stack_cubes(e):
+    """Cube 2 at rest on top of cube 1 (face to face, cube size 0.04 m)."""
+    for k in range(3):
+        e.obj[1].pos[k] = e.obj[0].pos[k] + (0.04 if k == 2 else 0.0)
+        e.obj[1].vel[k] = e.obj[1].omg[k] = 0.0
+    for k in range(4):
+        e.obj[1].quat[k] = e.obj[0].quat[k]
+
+
 def classify_workload(task, control, workload, mutation_name, B=64, steps=None, stride=1):
     """Class counts of every (env, step) sample of a workload whose GPU
     stand-in carries `mutation_name` (MUTATIONS).  Returns (counts, worst
@@ -135,7 +151,10 @@ def classify_workload(task, control, workload, mutation_name, B=64, steps=None, 
     for i in range(B):
         e = O.new_env(cfg)
         O.reset(cfg, e, seed=seed0 + i)
+        if workload == "stack_push":
+            stack_cubes(e)
         envs.append(e)
+    body = 1 if workload == "stack_push" else 0
     adim = O.action_dim(cfg)
     groups = groups_for(task, 7 if task in FREE_GRIPPER else 6)
     rng = np.random.default_rng(7)
@@ -148,7 +167,7 @@ def classify_workload(task, control, workload, mutation_name, B=64, steps=None, 
         if workload == "random":
             a = rng.uniform(-1, 1, size=(B, adim)).astype(np.float32)
         else:
-            a = _push_actions([oracle_env_from(cfg, snap, i) for i in range(B)], 0, s, adim, cfg)
+            a = _push_actions([oracle_env_from(cfg, snap, i) for i in range(B)], body, s, adim, cfg)
         for i in range(0, B, stride):
             gpu = oracle_env_from(cfg, snap, i)
             og, *_ = _stand_in_step(cfg, gpu, a[i], mutation)
@@ -174,4 +193,4 @@ def classify_workload(task, control, workload, mutation_name, B=64, steps=None, 
     return counts, worst, effect, visible
 
 
-__all__ = ["MUTATIONS", "classify_workload", "snapshot_of"]
+__all__ = ["MUTATIONS", "classify_workload", "snapshot_of", "stack_cubes"]

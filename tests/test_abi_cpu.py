@@ -197,3 +197,41 @@ def test_build_freshness_is_decided_by_content_not_mtime(tmp_path, monkeypatch):
     _lib.check_fresh(out)
     # flags are part of the stamp too
     assert B.fingerprint("") != B.fingerprint("prof") != B.fingerprint("", ["-DX"])
+
+
+def test_build_crash_retry_runs_alone():
+    """build._Scheduler: a crash retry starts only when no
+    compile is in flight, and no compile starts while it runs."""
+    import threading
+    import time
+
+    from pandasim import build as B
+
+    s = B._Scheduler()
+    log, seen = [], {}
+    s.start()  # a compile in flight
+
+    def retry():
+        seen["inflight"] = s._inflight
+        log.append("retry-start")
+        time.sleep(0.2)
+        log.append("retry-end")
+
+    t = threading.Thread(target=lambda: s.run_alone(retry))
+    t.start()
+    time.sleep(0.1)
+    assert log == []  # waits for the compile in flight
+    s.end()
+    time.sleep(0.05)
+
+    def late():
+        s.start()
+        log.append("late-start")
+        s.end()
+
+    u = threading.Thread(target=late)
+    u.start()
+    t.join()
+    u.join()
+    assert seen["inflight"] == 0
+    assert log == ["retry-start", "retry-end", "late-start"]

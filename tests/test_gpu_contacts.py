@@ -230,6 +230,15 @@ ULP_RUNS = 3
 # accepted cause of the lower fractions.
 FREE_RUN_FLOOR = {("push", "ee"): 0.82, ("pick_and_place", "ee"): 0.61,
                   ("reach", "joints"): 0.94, ("push", "joints"): 0.92}
+# Regression guard next to the yardstick floor: the GPU's own
+# fraction on the round-5 final library (profiles/r05at_pytest_gpu.log) less
+# 3 points.  The yardstick floor
+# says how far rounding alone may take the runs apart; this one fails a build
+# whose agreement drops well below what the path measured, e.g. PickAndPlace
+# falling 14 points to its floor.
+FREE_RUN_MEASURED = {("push", "ee"): 0.8788, ("pick_and_place", "ee"): 0.7516,
+                     ("reach", "joints"): 0.9642, ("push", "joints"): 0.9523}
+FREE_RUN_REGRESSION = 0.03
 _RUNS = {}
 
 
@@ -377,6 +386,7 @@ def test_free_running_200_steps(task, control):
     err_gpu, err_ulp, event, _, _ = _free_run(task, control)
     frac, frac_ulp = _report(task, control, err_gpu, err_ulp, event)
     assert frac >= FREE_RUN_FLOOR[(task, control)]
+    assert frac >= FREE_RUN_MEASURED[(task, control)] - FREE_RUN_REGRESSION
     assert frac >= frac_ulp - 0.02
 
 
@@ -385,6 +395,20 @@ def test_free_running_200_steps(task, control):
 # GPU's state before it, so a systematic difference on any contact
 # configuration the run reaches shows as a step error, where a free run only
 # shows chaos.  Bounds are test_gpu_parity's per-step ones.
+# The 200-step samples beyond the tight bounds on the product library, each
+# replayed from its dump (scripts/tf_sample.py, scripts/substep_compare.py,
+# profiles/r06c_substep_compare.log).  Round 5's 0.1 % allowance
+# is gone: any other beyond sample fails.  (Round 6's other one, Stack joints
+# step 64 env 44, is a box-box clip-line tie the classifier now recognises:
+# parity_judge._ill_conditioned's clip-bias probe.)
+TF200_EXEMPT = {
+    ("pick_and_place", "ee-random-gripper", 87, 15):
+        "the cube has left the table and slides (0.29 m/s) and spins on its side on the plane; its four "
+        "coplanar ground contacts are statically indeterminate, the GPU's and the oracle's normal impulses "
+        "among them part by 0.3-3 % from the first substep, and the spin error grows steadily to 2.5e-3 rad/s "
+        "(1.3 % of 0.19 rad/s; bound 2.26e-3) with positions within 6e-7 m; no oracle probe at fp32 "
+        "resolution (state noise, fp32 solver, PGS exit +-1..8 iterations) moves it beyond 1.4e-4 rad/s",
+}
 LONG_TF_CASES = [("reach", "joints"), ("push", "ee"), ("push", "joints"), ("pick_and_place", "ee"), ("slide", "ee"),
                  ("stack", "ee"), ("flip", "ee"),
                  # round 5: joint control of the other scenes, and a free gripper
@@ -398,10 +422,11 @@ def test_teacher_forced_200_steps(task, control):
     """64 envs x 200 steps, seed 2024 (the free runs' start): each GPU step vs
     one oracle step from the same state.  Samples beyond the tight bounds are
     dumped (state before and after, action, GPU observation) to
-    gpurun_out/tf200/ and listed; at most 0.1 % of env-steps may exceed them
-    (parity_judge.judge: beyond the tight bounds even after the oracle's
-    own sensitivity to the state's fp32 resolution is allowed for, and not at
-    a branch the oracle cannot resolve at that resolution), none the loose ones.
+    gpurun_out/tf200/ and listed; none may exceed them (parity_judge.judge:
+    beyond the tight bounds even after the oracle's own sensitivity to the
+    state's fp32 resolution is allowed for, and not at a branch the oracle
+    cannot resolve at that resolution) but the replayed ones of TF200_EXEMPT,
+    and no non-ill-conditioned one the loose ones.
     The free-gripper runs (PickAndPlace, Stack, Flip) hold the gripper half
     open (action 0), as in the event-onset test, so the finger-limit
     bifurcations stay out; the "ee-random-gripper" case keeps
@@ -452,7 +477,11 @@ def test_teacher_forced_200_steps(task, control):
                              gpu_obs=og[i], gpu_f_after=after[:, i], oracle_obs=o)
     print(task, control + (" (random gripper)" if random_gripper else ""), counts, "worst (not ill-conditioned)",
           {k: f"{v:.2e}" for k, v in worst.items()}, "beyond:", beyond[:20])
-    assert counts["beyond"] <= 0.001 * B * T
+    # no allowance: every beyond sample must be a listed,
+    # replayed one (TF200_EXEMPT)
+    name = control + ("-random-gripper" if random_gripper else "")
+    unexplained = [b for b in beyond if (task, name, b[0], b[1]) not in TF200_EXEMPT]
+    assert not unexplained, unexplained
     if random_gripper:
         assert counts["bif"] <= 0.08 * B * T and counts["conditioned"] <= 0.02 * B * T
     else:

@@ -550,6 +550,91 @@ def test_gripper_object_contact_parity(ps, task):
     assert e_obj.max() < 2e-2 and e_q.max() < SIM_LOOSE["q"] * 5
 
 
+# Contact-rich workloads classified like the random-action tests (round 6,
+# VERDICT r05 item 3): the ones tests/judge_power.py shows the classifier can
+# fail on -- Stack with cube 2 resting on cube 1 and the gripper dragging the
+# top cube over the bottom one ("stack_push": cube 2's mass and the cube-cube
+# friction x 1.02 are reported beyond), and the scripted push of Flip's cube
+# (its mass and friction x 1.02 move the quaternion observation beyond the
+# bounds).  The fp32 stand-in of tests/judge_power.py leaves 3.2 % (Stack)
+# and 2.9 % (Flip) of these samples conditioned and none beyond
+# (profiles/r06_judge_power.log); caps: 6 % conditioned, 8 % ill-conditioned,
+# 1 % ill-conditioned beyond the loose bounds.
+JUDGED_CONTACT_CAPS = {"conditioned": 0.06, "bif": 0.08}
+
+
+@pytest.mark.parametrize("task,workload", [("stack", "stack_push"), ("flip", "push"), ("stack", "push")])
+def test_judged_contact_workloads(ps, task, workload):
+    B, steps = 64, 14
+    env = make_env(ps, task, "ee", B)
+    env.autoreset = False
+    env.reset(seed=44)
+    if workload == "stack_push":
+        p1 = env.sim.get_base_position("object1").double()
+        p2 = p1.clone()
+        p2[:, 2] += 0.04  # cube 2 face to face on cube 1, at rest (judge_power.stack_cubes)
+        env.sim.set_base_pose("object2", p2, env.sim.get_base_orientation("object1").double())
+    body = {"stack_push": "object2", "push": "object1" if task == "stack" else "object"}[workload]
+    from test_gpu_contacts import _push_policy
+
+    policy = _push_policy(env, body)
+    cfg = oracle_config_for(env.sim.cfg)
+    groups = _groups(task, 7)
+    counts = {"tight": 0, "conditioned": 0, "bif": 0, "beyond": 0}
+    beyond, past_loose = [], []
+    p0 = env.sim.get_base_position(body).cpu().numpy()
+    for s in range(steps):
+        snap = snapshot(env.sim)
+        a = policy(s)
+        obs, *_ = env.step(torch.from_numpy(a).cuda())
+        og = obs["observation"].cpu().numpy()
+        after = None
+        for i in range(B):
+            o, *_ = O.step(cfg, oracle_env_from(cfg, snap, i), a[i])
+            cls, errs = _judge(cfg, snap, i, a[i], o, og[i], groups, task)
+            counts[cls] += 1
+            if cls == "beyond":
+                beyond.append((s, i, {k: f"{v:.1e}" for k, v in errs.items()}))
+                # dumped for scripts/tf_sample.py / substep_compare.py
+                after = env.sim.f[:, :B].double().cpu().numpy() if after is None else after
+                out = os.path.join("gpurun_out", "judged")
+                os.makedirs(out, exist_ok=True)
+                np.savez(os.path.join(out, f"{task}_ee_{s}_{i}.npz"), f=snap["f"][:, i], goal=snap["goal"][:, i],
+                         rng=snap["rng"][:, i], elapsed=snap["elapsed"][i], action=a[i], gpu_obs=og[i],
+                         gpu_f_after=after[:, i], oracle_obs=o)
+            if cls == "bif" and any(v > LOOSE[k] for k, v in errs.items()):
+                past_loose.append((s, i, {k: f"{v:.1e}" for k, v in errs.items() if v > LOOSE[k]}))
+    moved = np.linalg.norm(env.sim.get_base_position(body).cpu().numpy() - p0, axis=1)
+    print(task, workload, counts, f"moved {np.mean(moved > 1e-3) * 100:.0f} %", "beyond", beyond[:8],
+          "ill-conditioned past the loose bounds", past_loose)
+    assert np.mean(moved > 1e-3) > 0.5  # the gripper did reach the cube
+    n = B * steps
+    # Resting stacked cubes: a body's velocity after the solve is fixed only
+    # to the PGS stopping rule's resolution (Bullet exits once every row's
+    # (dl / dinv)^2 <= 1e-7: a last row velocity change of up to 3.2e-4 m/s,
+    # 1.6e-2 rad/s over the cube's 0.02 m contact offsets), and each of the
+    # two runs stops somewhere within it: twice that between them.  Replayed
+    # (round 6, stack_push steps 2 and 5, envs 9 and 22: the oracle's own
+    # probes move them by <= 1.4e-3 rad/s): positions and rotations agree to
+    # 3e-7 m / 2e-5 rad, velocities part by at most 3.7e-4 m/s and 1.2e-2
+    # rad/s.  Such samples (every other group tight, the objects' velocities
+    # within 6.4e-4 m/s and 3.2e-2 rad/s) are counted apart, at most 0.5 %; no
+    # other beyond.
+    def at_resolution(errs):
+        objv = [k for k in errs if k.startswith("obj") and k.endswith(("_vel", "_avel"))]
+        return all(v <= TOL[task][k] for k, v in errs.items() if k not in objv) and \
+            all(errs[k] <= (6.4e-4 if k.endswith("_vel") else 3.2e-2) for k in objv)
+    resolution = [b for b in beyond if at_resolution({k: float(v) for k, v in b[2].items()})]
+    assert len(beyond) == len(resolution), [b for b in beyond if b not in resolution]
+    assert len(resolution) <= 0.005 * n
+    assert counts["conditioned"] <= JUDGED_CONTACT_CAPS["conditioned"] * n
+    assert counts["bif"] <= JUDGED_CONTACT_CAPS["bif"] * n
+    # a cube balanced on an edge of the other (tipping) is a branch the oracle
+    # cannot resolve at fp32 resolution; where it tips the two runs part by
+    # more than the loose bounds (round 6: stack_push step 8 env 25)
+    assert len(past_loose) <= 0.01 * n
+
+
 @pytest.mark.parametrize("B,lanes", [(1, 1), (70, 1), (1, 16), (7, 16), (70, 16), (1, 8), (13, 8), (70, 8)])
 def test_ragged_batch_parity(ps, B, lanes):
     """Batches that are not a multiple of the wave (one env; 70 = a full

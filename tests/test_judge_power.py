@@ -23,7 +23,9 @@ B = 16  # envs per workload here; the committed scan uses the GPU tests' 64
 
 @pytest.mark.parametrize("task,control,workload", [("push", "ee", "random"), ("reach", "joints", "random"),
                                                    ("pick_and_place", "ee", "random"), ("push", "ee", "push"),
-                                                   ("slide", "ee", "push")])
+                                                   ("slide", "ee", "push"), ("stack", "ee", "random"),
+                                                   ("flip", "ee", "random"), ("stack", "ee", "stack_push"),
+                                                   ("flip", "ee", "push")])
 def test_unmutated_fp32_oracle_has_no_beyond_samples(task, control, workload):
     counts, *_ = J.classify_workload(task, control, workload, "none", B=B)
     print(task, control, workload, counts)
@@ -53,6 +55,33 @@ def test_model_errors_are_beyond(task, control, workload, mutation):
     assert visible > 0
     assert counts["beyond"] > 0
     assert counts["beyond"] >= 0.5 * visible
+
+
+# Round 6: the second cube and the cube-cube rows of
+# Stack, and Flip's quaternion observation.  At the GPU tests' 64 envs: with 16
+# the pair-friction case has too few visible samples for the half-beyond
+# criterion to be a measurement (10 of 26 at 16 envs, 56 of 108 at 64:
+# profiles/r06_judge_power.log).
+@pytest.mark.parametrize("task,control,workload,mutation", [
+    ("stack", "ee", "stack_push", "cube2_mass_x1.02"),
+    ("stack", "ee", "stack_push", "pair_friction_x1.02"),
+    ("stack", "ee", "stack_push", "cube_mass_x1.02"),
+    ("flip", "ee", "push", "cube_mass_x1.02"),
+    ("flip", "ee", "push", "cube_friction_0.51"),
+])
+def test_model_errors_are_beyond_stack_flip(task, control, workload, mutation):
+    counts, worst, effect, visible = J.classify_workload(task, control, workload, mutation, B=64)
+    print(task, control, workload, mutation, counts, f"samples the mutation moves beyond the tight bounds: {visible}",
+          {k: f"{v:.1e}" for k, v in effect.items()})
+    assert visible > 0
+    assert counts["beyond"] > 0
+    assert counts["beyond"] >= 0.5 * visible
+    if task == "flip":
+        # the mutation moves Flip's quaternion observation itself
+        assert effect["obj_rot"] > J.TOL["flip"]["obj_rot"]
+    if mutation in ("cube2_mass_x1.02", "pair_friction_x1.02"):
+        # ... and the second cube's, through the cube-cube rows
+        assert effect["obj2_pos"] > J.TOL["stack"]["obj2_pos"] and effect["obj2_rot"] > J.TOL["stack"]["obj2_rot"]
 
 
 def test_damping_error_on_a_motor_driven_arm_is_below_the_bounds():
