@@ -762,6 +762,13 @@ int ps_step(ps_ctx *c, void *state, const float *actions, float *obs, float *ag,
 }
 
 int ps_set_lanes_per_env(ps_ctx *c, int lanes) {
+#ifdef PS_EXPERIMENT_G2
+    // the two-lanes-per-env kernels of the experiment build
+    if (c && lanes == 2 && c->cfg.n_objects <= 1) {
+        c->lanes_per_env = lanes;
+        return PS_OK;
+    }
+#endif
     if (!c || !(lanes == 0 || lanes == 1 || lanes == 8 || lanes == 16)) return PS_ERR_ARG;
     if (lanes > 1 && c->cfg.n_objects > 1) return fail(c, PS_ERR_UNSUPPORTED, "8 or 16 lanes per env: one object at most");
     c->lanes_per_env = lanes;

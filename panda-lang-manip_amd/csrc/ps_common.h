@@ -325,6 +325,19 @@ PS_D float group8_bcast(float x) {
     return (__lane_id() & 8u) ? hi : lo;
 }
 
+// groups of 2 lanes (PS_EXPERIMENT_G2, DESIGN.md §12.13: two lanes per env):
+// the pair's other lane by quad_perm [1,0,3,2], the same bits in both lanes
+PS_D float group2_sum(float x) {
+#pragma clang fp contract(off)
+    return x + dpp_f<0xB1>(x);
+}
+// lane K of this lane's pair: quad_perm [K, K, K + 2, K + 2]
+template <int K>
+PS_D float group2_bcast(float x) {
+    static_assert(K == 0 || K == 1, "lane of the pair");
+    return dpp_f<K == 0 ? 0xA0 : 0xF5>(x);
+}
+
 // compile-time loop
 template <int B, int E, typename F>
 PS_D void static_for(F &&f) {

@@ -1599,12 +1599,14 @@ PS_D float cone_scale(float m2, float lim) {
 template <int G>
 PS_D float group_sum(float x) {
     if constexpr (G == 16) return group16_sum(x);
-    else return group8_sum(x);
+    else if constexpr (G == 8) return group8_sum(x);
+    else return group2_sum(x);
 }
 template <int G, int K>
 PS_D float group_bcast(float x) {
     if constexpr (G == 16) return group16_bcast<K>(x);
-    else return group8_bcast<K>(x);
+    else if constexpr (G == 8) return group8_bcast<K>(x);
+    else return group2_bcast<K>(x);
 }
 template <int NOBJ, int SHAPE, bool STD_MOTORS, int G>
 PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, unsigned gate_lim, unsigned lim_up,
@@ -1612,7 +1614,8 @@ PS_D void group_pgs(const Motors &mt, const float Mi[45], const MJStore &lds, un
                     const float lim_rhs[9], float lim_lam[9], const float mot_rhs[9], float mot_lam[9],
                     GroundContact gc[NG], RobotContact rc[NR], const BodyDyn<SHAPE> &od, float gmu, float dv[9],
                     V3 &dw, V3 &dvl PS_PROF_COUNT_PARAM PS_DUMP_PARAM) {
-    static_assert((G == 16 || G == 8) && NOBJ <= 1, "groups of 16 or 8 lanes hold 9 robot + 6 object DoFs");
+    // (G = 2: the PS_EXPERIMENT_G2 kernels, eight DoF slots per lane)
+    static_assert((G == 16 || G == 8 || G == 2) && NOBJ <= 1, "groups of 16, 8 or 2 lanes hold 9 robot + 6 object DoFs");
 #ifdef PS_DEBUG_ROW_DUMP
     int dk = 0;
     auto rec = [&](float x) {

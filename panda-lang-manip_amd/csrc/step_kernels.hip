@@ -7,6 +7,12 @@
 // DESIGN.md §12.6).
 #include "ps_env.h"
 
+#ifdef PS_EXPERIMENT_G2
+#define PS_G2_ENABLED 1
+#else
+#define PS_G2_ENABLED 0
+#endif
+
 #if !defined(PS_STEP_TASK) || !defined(PS_STEP_CONTROL)
 #error "build with -DPS_STEP_TASK=<task> -DPS_STEP_CONTROL=<control>"
 #endif
@@ -22,6 +28,13 @@ static_assert(PS_STEP_TASK != PS_TASK_STACK, "Stack has no group kernels (two ob
 int PS_STEP_GROUP_LAUNCHER_NAME(PS_STEP_TASK, PS_STEP_CONTROL)(ps_ctx *c, const void *params, const ps_step_io &io,
                                                                int lanes, hipStream_t st) {
     const KParams P = *static_cast<const KParams *>(params);
+#ifdef PS_EXPERIMENT_G2
+    // two lanes per env, a measured experiment only
+    if (lanes == 2) {
+        PS_LAUNCH(2);
+        return check_launch(c);
+    }
+#endif
     if (lanes == 16) PS_LAUNCH(16);
     else PS_LAUNCH(8);
     return check_launch(c);
@@ -39,7 +52,7 @@ int PS_STEP_LAUNCHER_NAME(PS_STEP_TASK, PS_STEP_CONTROL)(ps_ctx *c, void *state,
     P.write_gains = c->gains_dirty || state != c->gains_state;
     // groups of 16 or 8 lanes per env exist for the one-object and robot-only tasks
 #if PS_STEP_TASK != 4  // PS_TASK_STACK
-    if (lanes == 16 || lanes == 8)
+    if (lanes == 16 || lanes == 8 || (PS_G2_ENABLED && lanes == 2))
         return PS_STEP_GROUP_LAUNCHER_NAME(PS_STEP_TASK, PS_STEP_CONTROL)(c, &P, io, lanes, st);
 #endif
     PS_LAUNCH(1);

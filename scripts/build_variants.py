@@ -55,6 +55,11 @@ def _one_lane(units, flags_of_task):
 _TWO_WAVES = ["-DPS_EXPERIMENT_TWO_WAVES", "-DPS_STEP_MIN_WAVES=2"]
 
 UNIT_VARIANTS = {
+    # round 6: two lanes per env (group_pgs at G = 2, eight
+    # DoF slots per lane), the group objects register-allocated for two waves
+    # per SIMD; ps_set_lanes_per_env accepts 2 in this build only
+    "g2": lambda units: [(n, s, defs + ["-DPS_EXPERIMENT_G2"] + (["-DPS_STEP_MIN_WAVES=2"] if n.endswith("_groups") else []))
+                         for n, s, defs in units],
     # the group kernels (one LDS column per env since round 5) register-allocated
     # for two waves per SIMD
     "groups_2w": lambda units: [(n, s, defs + (["-DPS_STEP_MIN_WAVES=2"] if n.endswith("_groups") else []))

@@ -20,7 +20,7 @@ for cfg in ${PMC_CONFIGS:-$DEFAULT}; do
   run timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE $P -d ${d}_fetch -- python $BENCH > ${d}_fetch.log 2>&1
   run timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE $P -d ${d}_write -- python $BENCH > ${d}_write.log 2>&1
   run timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES $P -d ${d}_valu -- python $BENCH > ${d}_valu.log 2>&1
-  run timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 $P -d ${d}_fp32 -- python $BENCH > ${d}_fp32.log 2>&1
+  run timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP32_TRANS SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 $P -d ${d}_fp32 -- python $BENCH > ${d}_fp32.log 2>&1
 done
 cd $R
 echo "done rc=0"

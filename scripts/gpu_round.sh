@@ -36,7 +36,7 @@ if has pmc; then
   run timeout -s KILL 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE $P -d $R/gpurun_out/prof_fetch -- python $BENCH > $R/gpurun_out/prof_fetch.log 2>&1
   run timeout -s KILL 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE $P -d $R/gpurun_out/prof_write -- python $BENCH > $R/gpurun_out/prof_write.log 2>&1
   run timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES $P -d $R/gpurun_out/prof_valu -- python $BENCH > $R/gpurun_out/prof_valu.log 2>&1
-  run timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 $P -d $R/gpurun_out/prof_fp32 -- python $BENCH > $R/gpurun_out/prof_fp32.log 2>&1
+  run timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP32_TRANS SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 $P -d $R/gpurun_out/prof_fp32 -- python $BENCH > $R/gpurun_out/prof_fp32.log 2>&1
 fi
 cd $R
 if has phase; then

@@ -149,12 +149,23 @@ def main():
         sq = kernels[step[0]].get("sq_counters_per_launch", {})
         if "SQ_INSTS_VALU" in sq:
             traffic[args.workload]["valu_insts_per_launch"] = round(sq["SQ_INSTS_VALU"])
-        if "SQ_INSTS_VALU_FMA_F32" in sq:
-            # executed FP32 FLOPs: wave instructions x 64 lanes (FMA = 2), an upper
-            # bound when lanes are masked off (converged PGS lanes)
+        if "SQ_INSTS_VALU_FLOPS_FP32" in sq:
+            # executed FP32 FLOPs (round 6): gfx950's SQ_INSTS_VALU_FLOPS_FP32
+            # counts FLOPs per wave instruction with the packed ones at their
+            # width -- v_fma 2, v_add/v_mul 1, v_pk_fma 4, v_pk_add/v_pk_mul 2
+            # (calibrated: scripts/flops_probe.hip, profiles/r06c_flops_probe_counters.csv)
+            # -- x 64 lanes, plus the transcendental ones; an upper bound when
+            # lanes are masked off (converged PGS lanes)
+            traffic[args.workload]["fp32_flops_executed_per_launch"] = round(64 * (
+                sq["SQ_INSTS_VALU_FLOPS_FP32"] + sq.get("SQ_INSTS_VALU_FLOPS_FP32_TRANS", 0)))
+            traffic[args.workload]["fp32_flops_counter"] = "SQ_INSTS_VALU_FLOPS_FP32 (+_TRANS), packed included"
+        elif "SQ_INSTS_VALU_FMA_F32" in sq:
+            # older passes: instruction counts, where a v_pk_fma_f32 counts as one
+            # FMA (2 FLOPs, not 4): a lower bound for the packed solver loops
             traffic[args.workload]["fp32_flops_executed_per_launch"] = round(64 * (
                 2 * sq["SQ_INSTS_VALU_FMA_F32"] + sq.get("SQ_INSTS_VALU_ADD_F32", 0) +
                 sq.get("SQ_INSTS_VALU_MUL_F32", 0) + sq.get("SQ_INSTS_VALU_TRANS_F32", 0)))
+            traffic[args.workload]["fp32_flops_counter"] = "SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32: packed counted as scalar
         json.dump(traffic, open(tpath, "w"), indent=1)
     for k, e in sorted(kernels.items(), key=lambda kv: -kv[1]["avg_ns_all"] * kv[1]["launches"])[:4]:
         print(k, {x: (round(v, 1) if isinstance(v, float) else v) for x, v in e.items()
