@@ -2235,9 +2235,19 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         }
         mass_matrix(k, Mi);
     }
+#ifdef PS_PROFILE_PHASES
+    // (diagnostic build: M and M^-1 are forced out where their phases end;
+    // the product sinks them into the candidate code)
+#pragma unroll
+    for (int k = 0; k < 45; k++) asm volatile("" ::"v"(Mi[k]));
+#endif
     PS_PHASE(1);
     __builtin_amdgcn_sched_barrier(0);
     spd_inverse(Mi);
+#ifdef PS_PROFILE_PHASES
+#pragma unroll
+    for (int k = 0; k < 45; k++) asm volatile("" ::"v"(Mi[k]));
+#endif
     PS_PHASE(2);
     __builtin_amdgcn_sched_barrier(0);
     // gripper contact candidates: geometry only, so they are found here, where

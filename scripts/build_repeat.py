@@ -4,8 +4,11 @@ the default job count) with the compiler crashes each one logged
 (pandasim/build.py writes them to pandasim/build/build_log.jsonl), one JSON
 line per build.
 
-  python scripts/build_repeat.py 5 > profiles/r05_build_log.jsonl
+  python scripts/build_repeat.py 5 > profiles/r06_build_log.jsonl
+
+(round 6: also the built library's own sha256, to show the builds are reproducible)
 """
+import hashlib
 import json
 import os
 import sys
@@ -30,7 +33,8 @@ def main():
         new = crashes()[before:]
         print(json.dumps({"build": i + 1, "forced": True, "jobs": B._jobs(), "units": len(B.UNITS),
                           "seconds": round(time.time() - t, 1), "compiler_crashes": len(new), "crash_log": new,
-                          "lib_sha256_stamp": B.read_stamp(B.OUT)}), flush=True)
+                          "lib_sha256_stamp": B.read_stamp(B.OUT),
+                          "lib_file_sha256": hashlib.sha256(open(B.OUT, "rb").read()).hexdigest()}), flush=True)
 
 
 if __name__ == "__main__":
