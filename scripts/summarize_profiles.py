@@ -165,7 +165,7 @@ def main():
             traffic[args.workload]["fp32_flops_executed_per_launch"] = round(64 * (
                 2 * sq["SQ_INSTS_VALU_FMA_F32"] + sq.get("SQ_INSTS_VALU_ADD_F32", 0) +
                 sq.get("SQ_INSTS_VALU_MUL_F32", 0) + sq.get("SQ_INSTS_VALU_TRANS_F32", 0)))
-            traffic[args.workload]["fp32_flops_counter"] = "SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32: packed counted as scalar
+            traffic[args.workload]["fp32_flops_counter"] = "SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32: packed counted as scalar"
         json.dump(traffic, open(tpath, "w"), indent=1)
     for k, e in sorted(kernels.items(), key=lambda kv: -kv[1]["avg_ns_all"] * kv[1]["launches"])[:4]:
         print(k, {x: (round(v, 1) if isinstance(v, float) else v) for x, v in e.items()
