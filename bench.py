@@ -207,8 +207,9 @@ def fp32_roofline(work: dict, n_objects: int, env_steps_per_s_per_gpu: float) ->
     achieved = f["flops_per_env_step"] * env_steps_per_s_per_gpu / 1e12
     return dict(f, achieved_tflops=round(achieved, 3), peak_tflops=VALU_PEAK_TFLOPS,
                 frac=round(achieved / VALU_PEAK_TFLOPS, 4), unit="TFLOP/s",
-                note="peak = packed-FMA vector peak; the kernel issues scalar v_fma_f32 (half of it), "
-                     "and the PGS runs to the wave's slowest env (the counts are each env's own)")
+                note="algorithmic FLOPs (each env's own PGS iterations) over the packed-FMA vector peak; "
+                     "the kernel mixes scalar v_fma_f32 with v_pk_fma_f32 (DESIGN.md 12.12) and runs the PGS "
+                     "to the wave's slowest env: roofline.fp32_executed has the counted work")
 
 
 def file_sha256(path: str):
@@ -409,9 +410,9 @@ def main():
         out["roofline"]["fp32_executed"] = {
             "achieved_tflops": round(rate, 3), "peak_tflops": VALU_PEAK_TFLOPS, "frac": round(rate / VALU_PEAK_TFLOPS, 4),
             "flops_per_launch": executed,
-            "source": "profiles/pmc_traffic.json (SQ_INSTS_VALU_{FMA,ADD,MUL,TRANS}_F32 x 64 lanes, FMA = 2)",
-            "note": "a lower bound: the packed v_pk_{fma,mul,add}_f32 of the solver (DESIGN.md 12.12) are not "
-                    "in these counters (they fell by about two per packed instruction when the rows were packed)"}
+            "source": "profiles/pmc_traffic.json: " + pmc.get("fp32_flops_counter", "SQ_INSTS_VALU_*_F32") +
+                      ", x 64 lanes",
+            "packed_included": "packed included" in pmc.get("fp32_flops_counter", "")}
     if rank == 0:
         ep = episode_stats.double().cpu()
         done = ep[2] > 0
@@ -432,10 +433,13 @@ def main():
             if world > 1 or args.no_cpu_baseline:
                 out["roofline"]["fp32"]["work_source"] = WORK_COUNTS
             ex = out["roofline"].get("fp32_executed")
-            if ex:
+            if ex and ex["packed_included"]:
                 # executed (PMC) over algorithmic FLOPs per launch: the share of
                 # issue spent on lanes whose env has already converged, gated
-                # rows a lane lacks, and the like
+                # rows a lane lacks, and the like -- only from a
+                # counter that weighs the packed instructions right (round 6:
+                # SQ_INSTS_VALU_FLOPS_FP32; the old instruction counters took a
+                # v_pk_fma_f32 for one FMA)
                 algo = out["roofline"]["fp32"]["flops_per_env_step"] * B
                 ex["executed_over_algorithmic"] = round(ex["flops_per_launch"] / algo, 3)
         print(json.dumps(out), flush=True)
