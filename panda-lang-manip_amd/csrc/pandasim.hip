@@ -15,6 +15,21 @@ unsigned long long *ps_prof_buffer() {
         (void)hipMemset(g_prof, 0, sizeof(unsigned long long) * PS_NUM_PROF_SLOTS);
     return g_prof;
 }
+// per-env PGS iterations of each one-lane kernel launch's 20 substeps: 5 words
+// x PS_ITER_DUMP_ENVS, 8 bits per substep (PhaseTimer::itp)
+static uint32_t *g_itdump = nullptr;
+uint32_t *ps_iter_dump_buffer() {
+    if (!g_itdump && hipMalloc((void **)&g_itdump, sizeof(uint32_t) * 5 * PS_ITER_DUMP_ENVS) == hipSuccess)
+        (void)hipMemset(g_itdump, 0, sizeof(uint32_t) * 5 * PS_ITER_DUMP_ENVS);
+    return g_itdump;
+}
+extern "C" int ps_debug_env_iters(uint32_t *out) {
+    uint32_t *b = ps_iter_dump_buffer();
+    if (!b || hipDeviceSynchronize() != hipSuccess) return PS_ERR_HIP;
+    if (hipMemcpy(out, b, sizeof(uint32_t) * 5 * PS_ITER_DUMP_ENVS, hipMemcpyDeviceToHost) != hipSuccess)
+        return PS_ERR_HIP;
+    return PS_OK;
+}
 extern "C" int ps_debug_phase_cycles(unsigned long long *out, int reset) {
     unsigned long long *b = ps_prof_buffer();
     if (!b || hipDeviceSynchronize() != hipSuccess) return PS_ERR_HIP;

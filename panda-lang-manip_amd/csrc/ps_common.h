@@ -31,6 +31,9 @@
 // cost the instrumented kernel another PS_NUM_PROF_SLOTS VGPRs at 512)
 struct PhaseTimer {
     uint32_t last, acc[PS_NUM_PROF_SLOTS];
+    // the lane's PGS iterations of the last 20 substeps, 8 bits each, newest
+    // in the low byte of itp[0] (one-lane kernels; scripts/iter_dump.py)
+    uint32_t itp[5];
 };
 #define PS_PROF_PARAM , PhaseTimer &pt
 #define PS_PROF_ARG , pt

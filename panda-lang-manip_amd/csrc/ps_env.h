@@ -73,6 +73,8 @@ PS_DECLARE_SIM_LAUNCHER(2, 0)
 // the phase-counter buffer of the diagnostic build (pandasim.hip)
 #ifdef PS_PROFILE_PHASES
 unsigned long long *ps_prof_buffer();
+#define PS_ITER_DUMP_ENVS 131072
+uint32_t *ps_iter_dump_buffer();
 #endif
 #ifdef PS_DEBUG_ROW_DUMP
 float *ps_row_dump_buffer();
@@ -169,6 +171,7 @@ struct KParams {
     int64_t epstride;
 #ifdef PS_PROFILE_PHASES
     unsigned long long *prof;  // phase counters (ps_prof_buffer)
+    uint32_t *itdump;          // per-env PGS iterations of the last step (ps_iter_dump_buffer)
 #endif
 #ifdef PS_DEBUG_ROW_DUMP
     float *dbg;  // row dump (ps_row_dump_buffer)
@@ -585,6 +588,7 @@ inline KParams params_of(ps_ctx *c, void *state) {
     P.epstride = c->num_envs;
 #ifdef PS_PROFILE_PHASES
     P.prof = ps_prof_buffer();
+    P.itdump = ps_iter_dump_buffer();
 #endif
 #ifdef PS_DEBUG_ROW_DUMP
     P.dbg = ps_row_dump_buffer();
@@ -643,6 +647,7 @@ __global__ __launch_bounds__(kBlock, PS_STEP_MIN_WAVES) void k_step(KParams P, c
     PhaseTimer pt;
     pt.last = (uint32_t)__builtin_amdgcn_s_memtime();
     for (int k = 0; k < PS_NUM_PROF_SLOTS; k++) pt.acc[k] = 0;
+    for (int k = 0; k < 5; k++) pt.itp[k] = 0;
 #endif
     float q[9], qd[9];
     load_robot(s, i, q, qd);
@@ -762,6 +767,8 @@ __global__ __launch_bounds__(kBlock, PS_STEP_MIN_WAVES) void k_step(KParams P, c
     if ((threadIdx.x & 63) == 0)
         for (int k = 0; k < PS_NUM_PROF_SLOTS; k++)
             atomicAdd(&P.prof[k], (unsigned long long)pt.acc[k]);
+    if (G == 1 && P.itdump && i < PS_ITER_DUMP_ENVS)
+        for (int k = 0; k < 5; k++) P.itdump[(int64_t)k * PS_ITER_DUMP_ENVS + i] = pt.itp[k];
 #endif
 }
 

@@ -3275,6 +3275,9 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         }
         pt.acc[8] += prof_it;
         pt.acc[9] += wmax;
+#pragma unroll
+        for (int k = 4; k > 0; k--) pt.itp[k] = (pt.itp[k] << 8) | (pt.itp[k - 1] >> 24);
+        pt.itp[0] = (pt.itp[0] << 8) | (uint32_t)min(prof_it, 255);
         pt.acc[10] += 1;
         pt.acc[11] += wnr;
         // the wave's open row gates (wave-uniform: every lane adds the same)
