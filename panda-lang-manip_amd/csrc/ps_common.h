@@ -280,6 +280,44 @@ template <int CTRL>
 PS_D float dpp_f(float x) {
     return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), CTRL, 0xF, 0xF, true));
 }
+// The step kernels' logical block (round 6).  A group kernel's wave covers
+// 64 / G envs, so T = G / 2 consecutive waves share each 128-byte line of a
+// state row; blocks are observed to go round-robin over the 8 XCDs (b and
+// b + 8 share one, MI355X_MICROARCH.md), so those waves sat on different XCDs
+// and each XCD's L2 fetched the line again: FETCH 934 B per env-step at 8 lanes
+// and 1 424 B at 16 against 210 and 161 on one lane (profiles/r06m_*).  Two
+// bijective remaps put a line's waves on one XCD: the whole range (the blocks
+// of one XCD take consecutive envs) and tiles (runs of T consecutive waves on
+// one XCD, the runs dealt over the XCDs in turn).  Timed on the same sources
+// (profiles/r06o_ab.log, r06p_ab.log, three rotations each), the whole-range
+// remap costs 0.9 % at 8 lanes and nothing at 16, the tiles nothing at 8 and
+// 1.2 % at 16: the product takes tiles at 8 lanes and the whole range at 16.
+// Speed only: an env's results do not depend on the wave it runs in (the
+// group tests and scripts/compare_libs.py, bit for bit).
+// PS_XCD_REMAP (scripts/build_variants.py): 0 none, 1 the product's choice,
+// 2 the whole range at 8 and 16 lanes, 3 tiles at 8 and 16 lanes.
+#ifndef PS_XCD_REMAP
+#define PS_XCD_REMAP 1
+#endif
+template <int G>
+PS_D uint32_t step_block() {
+    const uint32_t b = blockIdx.x;
+    constexpr bool TILES = (PS_XCD_REMAP == 1 && G == 8) || PS_XCD_REMAP == 3;
+    if constexpr (G == 1 || PS_XCD_REMAP == 0) {
+        return b;
+    } else if constexpr (TILES) {
+        // the blocks past the last whole run of 8 T keep their order
+        constexpr uint32_t T = G / 2;
+        const uint32_t whole = gridDim.x / (8u * T) * (8u * T);
+        if (b >= whole) return b;
+        const uint32_t x = b % 8u, j = b / 8u;
+        return ((j / T) * 8u + x) * T + j % T;
+    } else {
+        const uint32_t n = gridDim.x, q = n / 8u, r = n % 8u, x = b % 8u;
+        return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + b / 8u;
+    }
+}
+
 // The additions are kept out of FMA contraction: with one DoF per lane the
 // summand is a product, and contracting `J v + dpp(J v)` into fma(J, v, dpp)
 // rounds this lane's term differently from the partner's copy of it, so the

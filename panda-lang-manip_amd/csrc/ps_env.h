@@ -637,7 +637,7 @@ __global__ __launch_bounds__(kBlock, PS_STEP_MIN_WAVES) void k_step(KParams P, c
                                                  float *reward, uint8_t *terminated, uint8_t *truncated,
                                                  float *final_obs, float *final_ag) {
     using T = TaskTraits<TASK>;
-    const int64_t gi = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+    const int64_t gi = ((int64_t)step_block<G>() * blockDim.x + threadIdx.x) / G;
     if (G == 1 && gi >= P.n) return;
     const bool live = gi < P.n;
     const int64_t i = live ? gi : P.n - 1;

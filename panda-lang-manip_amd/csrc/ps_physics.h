@@ -1513,7 +1513,7 @@ PS_D float joint_viol(float dl, float den) { return fmaf(fabsf(dl), den, -kResid
 // Addresses are re-derived at each access from wave-uniform values (row base,
 // stride, the wave's first env) and the lane id (v_mbcnt), so no per-lane
 // pointer or index stays live through the solve.  The step kernels run one
-// 64-lane wave per workgroup with G lanes per env, so env = (blockIdx.x * 64
+// 64-lane wave per workgroup with G lanes per env, so env = (step_block * 64
 // + lane) / G.  With G > 1 every lane of a group computes the same values;
 // lanes of a group past the batch end (live = false) compute a copy of the
 // last env and store nothing.
@@ -1531,7 +1531,7 @@ struct WarmCache {
     PS_D float &at(int row) const {
         // a 32-bit byte offset from a wave-uniform row base (ps_create caps
         // the batch at PS_MAX_ENVS), as StateView
-        const uint32_t e = (uint32_t)(((uint64_t)blockIdx.x * 64 + __lane_id()) / G) * 4u;
+        const uint32_t e = (uint32_t)(((uint64_t)step_block<G>() * 64 + __lane_id()) / G) * 4u;
         return *(float *)((char *)(base + (int64_t)(row - PS_F_WG0) * stride) + e);
     }
     PS_D float load(int row) const {

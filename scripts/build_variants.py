@@ -10,6 +10,11 @@ sys.path.insert(0, os.path.join(ROOT, "panda-lang-manip_amd"))
 from pandasim import build as B  # noqa: E402
 
 VARIANTS = {
+    # round 6: the group kernels' XCD-aware block order (ps_common.h step_block):
+    # none, the whole range at 8 and 16 lanes, tiles at 8 and 16 lanes
+    "noremap": ["-DPS_XCD_REMAP=0"],
+    "remapwhole": ["-DPS_XCD_REMAP=2"],
+    "remaptile": ["-DPS_XCD_REMAP=3"],
     "base": [],
     "maxilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
     "bias0": ["-mllvm", "-amdgpu-schedule-metric-bias=0"],
