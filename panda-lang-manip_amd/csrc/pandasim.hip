@@ -15,18 +15,19 @@ unsigned long long *ps_prof_buffer() {
         (void)hipMemset(g_prof, 0, sizeof(unsigned long long) * PS_NUM_PROF_SLOTS);
     return g_prof;
 }
-// per-env PGS iterations of each one-lane kernel launch's 20 substeps: 5 words
-// x PS_ITER_DUMP_ENVS, 8 bits per substep (PhaseTimer::itp)
+// per-env PGS iterations and contact slots of each one-lane kernel launch's 20
+// substeps: PS_ITP_WORDS words x PS_ITER_DUMP_ENVS, 16 bits per substep
+// (PhaseTimer::itp)
 static uint32_t *g_itdump = nullptr;
 uint32_t *ps_iter_dump_buffer() {
-    if (!g_itdump && hipMalloc((void **)&g_itdump, sizeof(uint32_t) * 5 * PS_ITER_DUMP_ENVS) == hipSuccess)
-        (void)hipMemset(g_itdump, 0, sizeof(uint32_t) * 5 * PS_ITER_DUMP_ENVS);
+    if (!g_itdump && hipMalloc((void **)&g_itdump, sizeof(uint32_t) * PS_ITP_WORDS * PS_ITER_DUMP_ENVS) == hipSuccess)
+        (void)hipMemset(g_itdump, 0, sizeof(uint32_t) * PS_ITP_WORDS * PS_ITER_DUMP_ENVS);
     return g_itdump;
 }
 extern "C" int ps_debug_env_iters(uint32_t *out) {
     uint32_t *b = ps_iter_dump_buffer();
     if (!b || hipDeviceSynchronize() != hipSuccess) return PS_ERR_HIP;
-    if (hipMemcpy(out, b, sizeof(uint32_t) * 5 * PS_ITER_DUMP_ENVS, hipMemcpyDeviceToHost) != hipSuccess)
+    if (hipMemcpy(out, b, sizeof(uint32_t) * PS_ITP_WORDS * PS_ITER_DUMP_ENVS, hipMemcpyDeviceToHost) != hipSuccess)
         return PS_ERR_HIP;
     return PS_OK;
 }
@@ -683,6 +684,7 @@ int ps_create(const ps_config *cfg, int64_t num_envs, int device, ps_ctx **out) 
     c->num_envs = num_envs;
     c->device = device;
     c->gains_dirty = 1;
+    c->env_packing = 1;
     ps_state_layout(num_envs, &c->lay);
     *out = c;
     return PS_OK;
@@ -691,6 +693,7 @@ int ps_create(const ps_config *cfg, int64_t num_envs, int device, ps_ctx **out) 
 void ps_destroy(ps_ctx *ctx) {
     if (ctx && ctx->render_prims) (void)hipFree(ctx->render_prims);
     if (ctx && ctx->gstash) (void)hipFree(ctx->gstash);
+    if (ctx && ctx->lane_env) (void)hipFree(ctx->lane_env);
     delete ctx;
 }
 
@@ -787,6 +790,12 @@ int ps_set_lanes_per_env(ps_ctx *c, int lanes) {
     if (!c || !(lanes == 0 || lanes == 1 || lanes == 8 || lanes == 16)) return PS_ERR_ARG;
     if (lanes > 1 && c->cfg.n_objects > 1) return fail(c, PS_ERR_UNSUPPORTED, "8 or 16 lanes per env: one object at most");
     c->lanes_per_env = lanes;
+    return PS_OK;
+}
+
+int ps_set_env_packing(ps_ctx *c, int on) {
+    if (!c || (on != 0 && on != 1)) return PS_ERR_ARG;
+    c->env_packing = on;
     return PS_OK;
 }
 

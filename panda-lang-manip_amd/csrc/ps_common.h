@@ -26,14 +26,16 @@
                               // rows, stays in 3; 20-23: gripper bounding tests -- (env, box) pairs
                               // passing them and boxes passing for some env of the wave, box-object
                               // then box-ground)
+#define PS_ITP_WORDS 10
 #ifdef PS_PROFILE_PHASES
 // (32-bit: one kernel's wave-cycles per phase fit, and 64-bit accumulators
 // cost the instrumented kernel another PS_NUM_PROF_SLOTS VGPRs at 512)
 struct PhaseTimer {
     uint32_t last, acc[PS_NUM_PROF_SLOTS];
-    // the lane's PGS iterations of the last 20 substeps, 8 bits each, newest
-    // in the low byte of itp[0] (one-lane kernels; scripts/iter_dump.py)
-    uint32_t itp[5];
+    // the lane's last 20 substeps, 16 bits each, newest in the low half of
+    // itp[0]: PGS iterations (bits 0-7), gripper slots nr (8-10), box-box
+    // slots np (11-13) (one-lane kernels; scripts/iter_dump.py)
+    uint32_t itp[PS_ITP_WORDS];
 };
 #define PS_PROF_PARAM , PhaseTimer &pt
 #define PS_PROF_ARG , pt
@@ -299,22 +301,38 @@ PS_D float dpp_f(float x) {
 #ifndef PS_XCD_REMAP
 #define PS_XCD_REMAP 1
 #endif
+// Contact-aware env packing of the one-lane step kernel (round 6, ps_env.h
+// k_pack): the envs of each window of PS_PACK_W consecutive envs are dealt to
+// the window's PS_PACK_W / 64 waves; the window's waves sit on one XCD
+// (tiles of PS_PACK_W / 64 waves), so the lanes' gathered state accesses stay
+// in that XCD's L2.
+constexpr int PS_PACK_W = 1024;
+// runs of T consecutive logical blocks on one XCD, the runs dealt over the
+// XCDs in turn; the blocks past the last whole run of 8 T keep their order
+template <uint32_t T>
+PS_D uint32_t xcd_tiles(uint32_t b, uint32_t n) {
+    const uint32_t whole = n / (8u * T) * (8u * T);
+    if (b >= whole) return b;
+    const uint32_t x = b % 8u, j = b / 8u;
+    return ((j / T) * 8u + x) * T + j % T;
+}
+// the blocks of one XCD take consecutive logical blocks
+PS_D uint32_t xcd_whole(uint32_t b, uint32_t n) {
+    const uint32_t q = n / 8u, r = n % 8u, x = b % 8u;
+    return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + b / 8u;
+}
 template <int G>
-PS_D uint32_t step_block() {
+PS_D uint32_t step_block(bool packed = false) {
     const uint32_t b = blockIdx.x;
     constexpr bool TILES = (PS_XCD_REMAP == 1 && G == 8) || PS_XCD_REMAP == 3;
-    if constexpr (G == 1 || PS_XCD_REMAP == 0) {
+    if constexpr (G == 1) {
+        return packed ? xcd_tiles<PS_PACK_W / 64>(b, gridDim.x) : b;
+    } else if constexpr (PS_XCD_REMAP == 0) {
         return b;
     } else if constexpr (TILES) {
-        // the blocks past the last whole run of 8 T keep their order
-        constexpr uint32_t T = G / 2;
-        const uint32_t whole = gridDim.x / (8u * T) * (8u * T);
-        if (b >= whole) return b;
-        const uint32_t x = b % 8u, j = b / 8u;
-        return ((j / T) * 8u + x) * T + j % T;
+        return xcd_tiles<G / 2>(b, gridDim.x);
     } else {
-        const uint32_t n = gridDim.x, q = n / 8u, r = n % 8u, x = b % 8u;
-        return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + b / 8u;
+        return xcd_whole(b, gridDim.x);
     }
 }
 

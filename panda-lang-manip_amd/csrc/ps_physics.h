@@ -1514,7 +1514,7 @@ PS_D float joint_viol(float dl, float den) { return fmaf(fabsf(dl), den, -kResid
 // stride, the wave's first env) and the lane id (v_mbcnt), so no per-lane
 // pointer or index stays live through the solve.  The step kernels run one
 // 64-lane wave per workgroup with G lanes per env, so env = (step_block * 64
-// + lane) / G.  With G > 1 every lane of a group computes the same values;
+// + lane) / G, through the lane -> env map when the one-lane kernel packs.  With G > 1 every lane of a group computes the same values;
 // lanes of a group past the batch end (live = false) compute a copy of the
 // last env and store nothing.
 // Scenes with at most one object (IN_LDS) use rows WG0..WG0ID and WR..WRID
@@ -1527,11 +1527,14 @@ struct WarmCache {
     int64_t stride;
     bool live;
     MJStore lds;
+    const int32_t *perm;  // the one-lane kernel's lane -> env map (k_pack), or NULL
     PS_D static int slot(int row) { return row < PS_F_WG1 ? row - PS_F_WG0 : 5 + (row - PS_F_WR); }
     PS_D float &at(int row) const {
         // a 32-bit byte offset from a wave-uniform row base (ps_create caps
-        // the batch at PS_MAX_ENVS), as StateView
-        const uint32_t e = (uint32_t)(((uint64_t)step_block<G>() * 64 + __lane_id()) / G) * 4u;
+        // the batch at PS_MAX_ENVS), as StateView; with env packing the
+        // lane's env is read back from the map (an L1 hit) rather than held
+        const uint32_t l = (uint32_t)(((uint64_t)step_block<G>(perm != nullptr) * 64 + __lane_id()) / G);
+        const uint32_t e = (perm ? (uint32_t)perm[l] : l) * 4u;
         return *(float *)((char *)(base + (int64_t)(row - PS_F_WG0) * stride) + e);
     }
     PS_D float load(int row) const {
@@ -2655,7 +2658,13 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
 #pragma unroll
     for (int b = 0; b < NB; b++) gate_ground[b] = wave_bits([&](int c) { return c < ng[b]; }, NG);
     unsigned gate_pair = wave_bits([&](int c) { return c < np; }, NP);
+#ifdef PS_EXPERIMENT_NO_PAIR_ROWS
+    gate_pair = 0u;  // timing experiment only (wrong physics): Stack's solve without its box-box rows
+#endif
     unsigned gate_robot = wave_bits([&](int c) { return c < nr; }, NR);
+#ifdef PS_EXPERIMENT_NO_ROBOT_ROWS
+    gate_robot = 0u;  // timing experiment only (wrong physics): the solve without the gripper rows
+#endif
 
 #ifdef PS_PROFILE_PHASES
     int prof_it = 0;
@@ -3276,8 +3285,8 @@ PS_D void substep(const Scene &sc, float q[9], float qd[9], const Motors &mt, Bo
         pt.acc[8] += prof_it;
         pt.acc[9] += wmax;
 #pragma unroll
-        for (int k = 4; k > 0; k--) pt.itp[k] = (pt.itp[k] << 8) | (pt.itp[k - 1] >> 24);
-        pt.itp[0] = (pt.itp[0] << 8) | (uint32_t)min(prof_it, 255);
+        for (int k = PS_ITP_WORDS - 1; k > 0; k--) pt.itp[k] = (pt.itp[k] << 16) | (pt.itp[k - 1] >> 16);
+        pt.itp[0] = (pt.itp[0] << 16) | (uint32_t)min(prof_it, 255) | ((uint32_t)nr << 8) | ((uint32_t)np << 11);
         pt.acc[10] += 1;
         pt.acc[11] += wnr;
         // the wave's open row gates (wave-uniform: every lane adds the same)

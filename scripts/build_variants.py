@@ -15,6 +15,9 @@ VARIANTS = {
     "noremap": ["-DPS_XCD_REMAP=0"],
     "remapwhole": ["-DPS_XCD_REMAP=2"],
     "remaptile": ["-DPS_XCD_REMAP=3"],
+    # timing only (wrong physics): the diagnostic build without Stack's box-box rows
+    "prof_nopair": ["-DPS_PROFILE_PHASES", "-DPS_EXPERIMENT_NO_PAIR_ROWS"],
+    "prof_norobot": ["-DPS_PROFILE_PHASES", "-DPS_EXPERIMENT_NO_ROBOT_ROWS"],
     "base": [],
     "maxilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
     "bias0": ["-mllvm", "-amdgpu-schedule-metric-bias=0"],
