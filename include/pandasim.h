@@ -171,14 +171,6 @@ int ps_step(ps_ctx *ctx, void *state, const float *actions, float *obs, float *a
 int ps_set_lanes_per_env(ps_ctx *ctx, int lanes);
 int ps_step_lanes(const ps_ctx *ctx); /* the value ps_step uses */
 
-/* Env packing of the one-lane step kernel (no reference counterpart; a
- * performance switch): on (1, the default), each ps_step
- * first deals the envs of every window of 1 024 consecutive envs to the
- * window's waves in the order of their contact slots in the previous step, so
- * the waves whose envs hold no gripper or box-box contact skip those rows.
- * Results do not change, bit for bit; 0 keeps env i in lane i. */
-int ps_set_env_packing(ps_ctx *ctx, int on);
-
 /* gymnasium's RecordEpisodeStatistics, fused into ps_step (no reference
  * counterpart: the training loop's wrapper around gym.make).  stats != NULL:
  * device [4, B] f32, caller-owned, must outlive the steps: row 0 the running

@@ -684,7 +684,6 @@ int ps_create(const ps_config *cfg, int64_t num_envs, int device, ps_ctx **out) 
     c->num_envs = num_envs;
     c->device = device;
     c->gains_dirty = 1;
-    c->env_packing = 1;
     ps_state_layout(num_envs, &c->lay);
     *out = c;
     return PS_OK;
@@ -693,7 +692,6 @@ int ps_create(const ps_config *cfg, int64_t num_envs, int device, ps_ctx **out) 
 void ps_destroy(ps_ctx *ctx) {
     if (ctx && ctx->render_prims) (void)hipFree(ctx->render_prims);
     if (ctx && ctx->gstash) (void)hipFree(ctx->gstash);
-    if (ctx && ctx->lane_env) (void)hipFree(ctx->lane_env);
     delete ctx;
 }
 
@@ -790,12 +788,6 @@ int ps_set_lanes_per_env(ps_ctx *c, int lanes) {
     if (!c || !(lanes == 0 || lanes == 1 || lanes == 8 || lanes == 16)) return PS_ERR_ARG;
     if (lanes > 1 && c->cfg.n_objects > 1) return fail(c, PS_ERR_UNSUPPORTED, "8 or 16 lanes per env: one object at most");
     c->lanes_per_env = lanes;
-    return PS_OK;
-}
-
-int ps_set_env_packing(ps_ctx *c, int on) {
-    if (!c || (on != 0 && on != 1)) return PS_ERR_ARG;
-    c->env_packing = on;
     return PS_OK;
 }
 

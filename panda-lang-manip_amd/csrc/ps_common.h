@@ -301,12 +301,6 @@ PS_D float dpp_f(float x) {
 #ifndef PS_XCD_REMAP
 #define PS_XCD_REMAP 1
 #endif
-// Contact-aware env packing of the one-lane step kernel (round 6, ps_env.h
-// k_pack): the envs of each window of PS_PACK_W consecutive envs are dealt to
-// the window's PS_PACK_W / 64 waves; the window's waves sit on one XCD
-// (tiles of PS_PACK_W / 64 waves), so the lanes' gathered state accesses stay
-// in that XCD's L2.
-constexpr int PS_PACK_W = 1024;
 // runs of T consecutive logical blocks on one XCD, the runs dealt over the
 // XCDs in turn; the blocks past the last whole run of 8 T keep their order
 template <uint32_t T>
@@ -322,12 +316,10 @@ PS_D uint32_t xcd_whole(uint32_t b, uint32_t n) {
     return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + b / 8u;
 }
 template <int G>
-PS_D uint32_t step_block(bool packed = false) {
+PS_D uint32_t step_block() {
     const uint32_t b = blockIdx.x;
     constexpr bool TILES = (PS_XCD_REMAP == 1 && G == 8) || PS_XCD_REMAP == 3;
-    if constexpr (G == 1) {
-        return packed ? xcd_tiles<PS_PACK_W / 64>(b, gridDim.x) : b;
-    } else if constexpr (PS_XCD_REMAP == 0) {
+    if constexpr (G == 1 || PS_XCD_REMAP == 0) {
         return b;
     } else if constexpr (TILES) {
         return xcd_tiles<G / 2>(b, gridDim.x);

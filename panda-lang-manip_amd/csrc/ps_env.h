@@ -31,8 +31,6 @@ struct ps_ctx {
     int gains_dirty;      // the state's motor gain rows may differ from the fused step's (store_motor_gains)
     const void *gains_state;  // the state buffer whose gain rows the last successful ps_step wrote
     float *epstats;       // ps_set_episode_stats: caller-owned [4][num_envs] f32, or NULL
-    int env_packing;      // ps_set_env_packing: the one-lane step deals envs to waves by contact slots (default 1)
-    int32_t *lane_env;    // its lane -> env map, [num_envs], allocated on first use
 };
 
 // arguments of ps_step that the step launchers pass through
@@ -171,7 +169,6 @@ struct KParams {
     int write_gains;  // k_step also stores the motor gain rows (ps_ctx::gains_dirty)
     float *epstats;   // ps_set_episode_stats: [4][epstride] running return, last return, last success, episodes
     int64_t epstride;
-    const int32_t *lane_env;  // one-lane k_step: lane (slot) -> env (k_pack), or NULL = identity
 #ifdef PS_PROFILE_PHASES
     unsigned long long *prof;  // phase counters (ps_prof_buffer)
     uint32_t *itdump;          // per-env PGS iterations of the last step (ps_iter_dump_buffer)
@@ -276,7 +273,7 @@ template <int NOBJ, int SHAPE, bool STD_MOTORS, int G = 1>
 PS_D void run_substeps(const KParams &P, int64_t i, int n, float q[9], float qd[9], Body *bd,
                        const MJStore &lds, bool live, const float *tgt PS_PROF_PARAM) {
     static_assert(kBlock == 64, "WarmCache: one wave per workgroup");
-    const WarmCache<G, NOBJ> wc{P.s.f + PS_F_WG0 * P.s.stride, P.s.stride, live, lds, G == 1 ? P.lane_env : nullptr};
+    const WarmCache<G, NOBJ> wc{P.s.f + PS_F_WG0 * P.s.stride, P.s.stride, live, lds};
     wc.to_lds();
     // G > 1: the targets come back from the state rows, which every lane of
     // the group wrote with the same values (k_step); held in registers across
@@ -584,7 +581,6 @@ inline KParams params_of(ps_ctx *c, void *state) {
     P.action_dim = ps_action_dim(c);
     P.autoreset = 0;
     P.gstash = c->gstash;
-    P.lane_env = nullptr;
     P.nonfinite = nullptr;
     P.reset_nonfinite = 0;
     P.write_gains = 0;
@@ -623,15 +619,6 @@ inline int ensure_stash(ps_ctx *c, hipStream_t st) {
 
 inline dim3 grid_of(int64_t n, int block) { return dim3((unsigned)((n + block - 1) / block)); }
 
-// the one-lane step's lane -> env map (k_pack), allocated on first use
-inline int ensure_pack(ps_ctx *c) {
-    if (c->lane_env) return PS_OK;
-    if (hipMalloc((void **)&c->lane_env, sizeof(int32_t) * c->num_envs) != hipSuccess) {
-        c->lane_env = nullptr;
-        return PS_ERR_HIP;
-    }
-    return PS_OK;
-}
 
 // the registered scene of each task (its _create_scene + panda_tasks.py)
 inline bool scene_matches_task(const ps_config &c) {
@@ -639,55 +626,6 @@ inline bool scene_matches_task(const ps_config &c) {
            (c.n_objects == 0 || c.object_shape == (c.task == PS_TASK_SLIDE ? PS_SHAPE_CYLINDER : PS_SHAPE_BOX));
 }
 
-
-// Contact-aware env packing (round 6).  A wave runs a
-// contact slot's rows while any of its lanes has that slot (the gates of the
-// one-lane solver), and in the bench workload a third of the envs hold
-// gripper slots in a step, spread over every wave; an env's slots persist
-// from one step to the next (p = 0.76-0.79, profiles/r06x_iter_dump.log).
-// So before a one-lane step the envs of each window of PS_PACK_W consecutive
-// envs are dealt to the window's waves in the order of their slots in the
-// previous step's last substep -- the contact cache rows: gripper slots in
-// use (PS_F_WRID), box-box slots in use (PS_F_WPN, Stack) -- most first, in
-// env order within a key (a stable counting sort).  An env's results do not
-// depend on its wave, so they are the same bits (scripts/compare_libs.py).
-constexpr int PACK_KEYS = 8;
-__global__ __launch_bounds__(PS_PACK_W) void k_pack(StateView s, int64_t n, int pairs, int32_t *lane_env) {
-    __shared__ int cnt[PS_PACK_W / 64][PACK_KEYS];
-    __shared__ int base[PS_PACK_W / 64][PACK_KEYS];
-    const int64_t w0 = (int64_t)blockIdx.x * PS_PACK_W;
-    const int t = (int)threadIdx.x, wv = t >> 6, lane = t & 63;
-    const int64_t e = w0 + t;
-    const bool in = e < n;
-    int key = 0;
-    if (in) {
-        const unsigned pack = (unsigned)s.F(PS_F_WRID, e);
-        int nr = 0;
-#pragma unroll
-        for (int k = 0; k < NR; k++) nr += ((pack >> (5 * k)) & 31u) != 0u;
-        const int np = pairs ? (int)s.F(PS_F_WPN, e) : 0;
-        key = np > 0 ? min(NR + np, PACK_KEYS - 1) : nr;
-    }
-    const uint64_t below = (1ull << lane) - 1ull;
-    int rank = 0;
-#pragma unroll
-    for (int b = 0; b < PACK_KEYS; b++) {
-        const uint64_t m = __ballot(in && key == b);
-        if (key == b) rank = __popcll(m & below);
-        if (lane == 0) cnt[wv][b] = __popcll(m);
-    }
-    __syncthreads();
-    if (t == 0) {
-        int off = 0;
-        for (int b = PACK_KEYS - 1; b >= 0; b--)  // most slots first
-            for (int w = 0; w < PS_PACK_W / 64; w++) {
-                base[w][b] = off;
-                off += cnt[w][b];
-            }
-    }
-    __syncthreads();
-    if (in) lane_env[w0 + base[wv][key] + rank] = (int32_t)e;
-}
 
 // The fused env step: G lanes = one env = one full RobotTaskEnv.step().
 // G = 1: one env per lane (large batches).  G = 16 (small batches, NOBJ <= 1):
@@ -700,11 +638,10 @@ __global__ __launch_bounds__(kBlock, PS_STEP_MIN_WAVES) void k_step(KParams P, c
                                                  float *reward, uint8_t *terminated, uint8_t *truncated,
                                                  float *final_obs, float *final_ag) {
     using T = TaskTraits<TASK>;
-    const int64_t gi = ((int64_t)step_block<G>(G == 1 && P.lane_env) * blockDim.x + threadIdx.x) / G;
+    const int64_t gi = ((int64_t)step_block<G>() * blockDim.x + threadIdx.x) / G;
     if (G == 1 && gi >= P.n) return;
     const bool live = gi < P.n;
-    // gi: the lane's slot; i: its env (the slot itself, or the env k_pack dealt it)
-    const int64_t i = live ? (G == 1 && P.lane_env ? (int64_t)P.lane_env[gi] : gi) : P.n - 1;
+    const int64_t i = live ? gi : P.n - 1;
     const bool writer = G == 1 || (live && (threadIdx.x % G) == 0);
     const StateView &s = P.s;
 #ifdef PS_PROFILE_PHASES
@@ -740,12 +677,11 @@ __global__ __launch_bounds__(kBlock, PS_STEP_MIN_WAVES) void k_step(KParams P, c
     if constexpr (T::NOBJ == 2) {
         lds.gst = P.gstash;
         lds.gst_stride = s.stride;
-        // (the stash is the step's scratch: indexed by slot, coalesced whatever env the lane holds)
-        lds.goff = StateView::off(gi, 4);
+        lds.goff = StateView::off(i, 4);
         lds.gpair = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_PAIR_OFFSET * s.stride +
-                                                                 gi * (NP * PAIR_FLOATS));
+                                                                 i * (NP * PAIR_FLOATS));
         lds.ggrip = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_GRIP_OFFSET * s.stride +
-                                                                 gi * GRIP_FLOATS);
+                                                                 i * GRIP_FLOATS);
         lds.gzero = (__attribute__((address_space(1))) float *)(P.gstash + (int64_t)GSTASH_FLOATS * s.stride);
     }
 #ifdef PS_EXPERIMENT_TWO_WAVES

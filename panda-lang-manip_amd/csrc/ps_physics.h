@@ -1514,7 +1514,7 @@ PS_D float joint_viol(float dl, float den) { return fmaf(fabsf(dl), den, -kResid
 // stride, the wave's first env) and the lane id (v_mbcnt), so no per-lane
 // pointer or index stays live through the solve.  The step kernels run one
 // 64-lane wave per workgroup with G lanes per env, so env = (step_block * 64
-// + lane) / G, through the lane -> env map when the one-lane kernel packs.  With G > 1 every lane of a group computes the same values;
+// + lane) / G.  With G > 1 every lane of a group computes the same values;
 // lanes of a group past the batch end (live = false) compute a copy of the
 // last env and store nothing.
 // Scenes with at most one object (IN_LDS) use rows WG0..WG0ID and WR..WRID
@@ -1527,14 +1527,11 @@ struct WarmCache {
     int64_t stride;
     bool live;
     MJStore lds;
-    const int32_t *perm;  // the one-lane kernel's lane -> env map (k_pack), or NULL
     PS_D static int slot(int row) { return row < PS_F_WG1 ? row - PS_F_WG0 : 5 + (row - PS_F_WR); }
     PS_D float &at(int row) const {
         // a 32-bit byte offset from a wave-uniform row base (ps_create caps
-        // the batch at PS_MAX_ENVS), as StateView; with env packing the
-        // lane's env is read back from the map (an L1 hit) rather than held
-        const uint32_t l = (uint32_t)(((uint64_t)step_block<G>(perm != nullptr) * 64 + __lane_id()) / G);
-        const uint32_t e = (perm ? (uint32_t)perm[l] : l) * 4u;
+        // the batch at PS_MAX_ENVS), as StateView
+        const uint32_t e = (uint32_t)(((uint64_t)step_block<G>() * 64 + __lane_id()) / G) * 4u;
         return *(float *)((char *)(base + (int64_t)(row - PS_F_WG0) * stride) + e);
     }
     PS_D float load(int row) const {

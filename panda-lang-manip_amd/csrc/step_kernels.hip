@@ -55,12 +55,6 @@ int PS_STEP_LAUNCHER_NAME(PS_STEP_TASK, PS_STEP_CONTROL)(ps_ctx *c, void *state,
     if (lanes == 16 || lanes == 8 || (PS_G2_ENABLED && lanes == 2))
         return PS_STEP_GROUP_LAUNCHER_NAME(PS_STEP_TASK, PS_STEP_CONTROL)(c, &P, io, lanes, st);
 #endif
-    if (c->env_packing) {
-        if (ensure_pack(c) != PS_OK) return fail(c, PS_ERR_HIP, "env packing: hipMalloc failed");
-        hipLaunchKernelGGL(k_pack, grid_of(P.n, PS_PACK_W), dim3(PS_PACK_W), 0, st, P.s, P.n,
-                           (int)(c->cfg.n_objects == 2), c->lane_env);
-        P.lane_env = c->lane_env;
-    }
     PS_LAUNCH(1);
     return check_launch(c);
 }

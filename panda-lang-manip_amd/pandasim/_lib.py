@@ -62,20 +62,6 @@ class PandasimError(RuntimeError):
 _lib = None
 
 
-# symbols newer than the earlier rounds' libraries that scripts/time_variants.py
-# and compare_libs.py load for A/B runs (PANDASIM_LIB): such a library may lack
-# them (the host layer then skips the call); the product library may not
-OPTIONAL_SYMBOLS = ("ps_set_env_packing",)
-
-
-def _missing_optional(L, name: str) -> bool:
-    if name not in OPTIONAL_SYMBOLS or hasattr(L, name):
-        return False
-    if os.path.abspath(LIB_PATH) == os.path.abspath(os.path.join(HERE, "libpandasim.so")):
-        raise PandasimError(f"{LIB_PATH} lacks {name}: rebuild it with `python -m pandasim.build`")
-    return True
-
-
 def exported_symbols():
     return [
         "ps_abi_version", "ps_default_config", "ps_state_layout", "ps_create", "ps_destroy", "ps_last_error",
@@ -83,7 +69,7 @@ def exported_symbols():
         "ps_step", "ps_sim_step", "ps_link_state", "ps_inverse_kinematics", "ps_compute_reward", "ps_rng_seed",
         "ps_rng_uniform", "ps_rng_rotation", "ps_base_state", "ps_camera", "ps_render", "ps_deproject_image",
         "ps_deproject_pixels", "ps_set_nonfinite_guard", "ps_set_lanes_per_env", "ps_step_lanes",
-        "ps_mark_motor_rows_dirty", "ps_set_episode_stats", "ps_set_env_packing",
+        "ps_mark_motor_rows_dirty", "ps_set_episode_stats",
     ]
 
 
@@ -143,8 +129,6 @@ def lib():
     L.ps_set_nonfinite_guard.argtypes = [V, V, I]
     L.ps_set_lanes_per_env.argtypes = [V, I]
     L.ps_step_lanes.argtypes = [V]
-    if not _missing_optional(L, "ps_set_env_packing"):
-        L.ps_set_env_packing.argtypes = [V, I]
     L.ps_mark_motor_rows_dirty.argtypes = [V]
     L.ps_set_episode_stats.argtypes = [V, V]
     L.ps_link_state.argtypes = [V, V, I, V, V, V, V, V]
@@ -160,8 +144,6 @@ def lib():
     L.ps_deproject_image.argtypes = [V, V, D, I, I, V, V, V, V]
     L.ps_deproject_pixels.argtypes = [V, V, V, I, D, I, I, V, V]
     for name in exported_symbols():
-        if _missing_optional(L, name):
-            continue
         getattr(L, name).restype = getattr(L, name).restype if name in ("ps_destroy", "ps_last_error") else I
     _lib = L
     return L

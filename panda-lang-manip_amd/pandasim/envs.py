@@ -43,16 +43,12 @@ class PandaVecEnv:
     metadata = {"render_modes": ["rgb_array"]}
 
     def __init__(self, task: str, reward_type: str = "sparse", control_type: str = "ee", num_envs: int = 1,
-                 device="cuda", autoreset: bool = True, lanes_per_env: int = 0, env_packing: bool = True):
+                 device="cuda", autoreset: bool = True, lanes_per_env: int = 0):
         self.task_name, self.reward_type, self.control_type = task, reward_type, control_type
         self.sim = PandaSim(task, control_type, reward_type, num_envs, device)
         # 0: the library picks 16 or 8 lanes per env for small batches, 1 above (ps_set_lanes_per_env)
         self.sim._call("ps_set_lanes_per_env", self.sim._ctx, int(lanes_per_env))
         self.lanes_per_env = self.sim._lib.ps_step_lanes(self.sim._ctx)
-        # the one-lane kernel deals envs to waves by their contact slots (ps_set_env_packing;
-        # the same results bit for bit, fewer contact rows run by waves that have none)
-        if hasattr(self.sim._lib, "ps_set_env_packing"):  # (an earlier round's library under PANDASIM_LIB lacks it)
-            self.sim._call("ps_set_env_packing", self.sim._ctx, int(bool(env_packing)))
         self.num_envs = self.sim.num_envs
         self.device = self.sim.device
         self.autoreset = autoreset

@@ -26,7 +26,7 @@ def main():
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
     steps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
     lanes = int(sys.argv[4]) if len(sys.argv) > 4 else 0
-    env = pandasim.make(env_id, num_envs=B, lanes_per_env=lanes, env_packing=os.environ.get("PACKING", "1") == "1")
+    env = pandasim.make(env_id, num_envs=B, lanes_per_env=lanes)
     env.reset(seed=12345)
     lib = L.lib()
     lib.ps_debug_phase_cycles.argtypes = [C.c_void_p, C.c_int]

@@ -10,8 +10,7 @@ for task in os.environ.get("TASKS", "push").split(","):
     env_id = {"reach": "PandaReach-v3", "push": "PandaPush-v3", "pick_and_place": "PandaPickAndPlace-v3",
               "stack": "PandaStack-v3", "flip": "PandaFlip-v3", "slide": "PandaSlide-v3"}[task]
     B = int(os.environ.get("B", "65536"))
-    env = pandasim.make(env_id, num_envs=B, lanes_per_env=int(os.environ.get("LANES", "0")),
-                        env_packing=os.environ.get("PACKING", "1") == "1")
+    env = pandasim.make(env_id, num_envs=B, lanes_per_env=int(os.environ.get("LANES", "0")))
     env.reset(seed=12345)
     g = torch.Generator(device="cuda"); g.manual_seed(0)
     acts = torch.rand(30, B, env.action_dim, device="cuda", generator=g) * 2 - 1

@@ -39,10 +39,10 @@ def ps():
     return pandasim
 
 
-def make_env(ps, task, control, n, reward="sparse", lanes=0, packing=True):
+def make_env(ps, task, control, n, reward="sparse", lanes=0):
     from pandasim.envs import PandaVecEnv
 
-    return PandaVecEnv(task, reward, control, n, "cuda", lanes_per_env=lanes, env_packing=packing)
+    return PandaVecEnv(task, reward, control, n, "cuda", lanes_per_env=lanes)
 
 
 # ps_step kernels: one env per lane, and groups of 16 or 8 lanes per env (not Stack)
@@ -657,38 +657,6 @@ def test_ragged_batch_parity(ps, B, lanes):
             o, *_ = O.step(cfg, oracle_env_from(cfg, snap, i), a[i])
             for k, idx in groups.items():
                 assert np.abs(og[i, idx] - o[idx]).max() <= TOL["push"][k], (B, i, k)
-
-
-@pytest.mark.parametrize("task,control", [("push", "ee"), ("pick_and_place", "joints"), ("stack", "ee"),
-                                          ("flip", "ee")])
-def test_env_packing_is_bit_identical(ps, task, control):
-    """The one-lane kernel with env packing (k_pack deals each window of 1 024
-    envs to its waves by their contact slots) against env i in lane i: the
-    same seeds and actions give the same state bytes, observations, rewards
-    and flags at every step, bit for bit, through resets (an env's solve does
-    not depend on its wave).  5 000 envs: four whole windows and a ragged one;
-    after a few steps the packing moves envs between waves."""
-    B, steps = 5000, 16
-    envs = [make_env(ps, task, control, B, lanes=1, packing=p) for p in (True, False)]
-    for e in envs:
-        e.reset(seed=321)
-    g = torch.Generator(device="cuda")
-    g.manual_seed(7)
-    for k in range(steps):
-        a = torch.rand(B, envs[0].action_dim, device="cuda", generator=g) * 2 - 1
-        outs = [e.step(a) for e in envs]
-        torch.cuda.synchronize()
-        assert torch.equal(envs[0].sim.state, envs[1].sim.state), (task, k)
-        for x, y in zip(outs[0][:4], outs[1][:4]):
-            if isinstance(x, dict):
-                for key in x:
-                    assert torch.equal(x[key], y[key]), (task, k, key)
-            else:
-                assert torch.equal(x, y), (task, k)
-    # gripper contact slots were in use in some envs and not in others, so the
-    # packing did deal envs away from their own lanes
-    rid = envs[0].sim.f[103, :B]  # PS_F_WRID (include/pandasim.h)
-    assert 0 < int((rid != 0).sum()) < B, task
 
 
 GROUP_TASKS = [(t, c) for t, c in TASKS if t != "stack"]
