@@ -662,8 +662,9 @@ def test_ragged_batch_parity(ps, B, lanes):
 GROUP_TASKS = [(t, c) for t, c in TASKS if t != "stack"]
 
 
+@pytest.mark.parametrize("B", [64, 1000])
 @pytest.mark.parametrize("task,control", GROUP_TASKS)
-def test_group_kernels_match_one_lane(ps, task, control):
+def test_group_kernels_match_one_lane(ps, task, control, B):
     """The 16- and 8-lane group kernels against the one-lane kernel over the
     same step from the same reset (no gripper contact yet): the robot's rows
     (q, qd: rows 0-17) of every env equal bit for bit, every other row within
@@ -673,8 +674,10 @@ def test_group_kernels_match_one_lane(ps, task, control):
     pairs 0.0 apart in q, qd).  Round 3's -O3 Slide group kernels were off by
     6.8e-3 to 2.1e-1 rad/s in the joint velocities; any such
     recurrence, or codegen drift, fails here.  Contact states:
-    test_group_kernels_match_one_lane_in_contact."""
-    B = 64
+    test_group_kernels_match_one_lane_in_contact.  1 000 envs: 125 and 250
+    group blocks, so the XCD-aware block order (ps_common.h step_block:
+    tiles of 4 waves at 8 lanes up to block 96, then the blocks' own order;
+    the whole range at 16) maps every env to one group, each once."""
     res = {}
     for lanes in (1, 8, 16):
         env = make_env(ps, task, control, B, lanes=lanes)
